@@ -1,0 +1,117 @@
+/*
+ * tbg.h — C ABI of the MI355X batch-apply engine (libtbgpu.so).
+ *
+ * The engine replaces the body of the reference StateMachine's commit path for create_accounts,
+ * create_transfers and pulse (src/state_machine.zig:543-1306, 1421-1929). Each entry point names
+ * the reference interface it stands in for. Plain pointers and sizes only; all functions return
+ * 0 on success and a negative status on failure. A failure is fatal for the caller (the reference
+ * `commit` is infallible, state_machine.zig:1107-1115; device errors must panic the replica), and
+ * the engine never partially applies a batch it rejected up front (bad input, capacity).
+ *
+ * Threading: an engine is driven by one host thread at a time (the replica event loop,
+ * state_machine.zig:606-607: one prefetch or commit in flight).
+ */
+#ifndef TBG_H
+#define TBG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "tb_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tbg_engine tbg_engine;
+
+typedef struct tbg_config {
+    int32_t device;          /* HIP device ordinal */
+    uint32_t batch_max;      /* constants.batch_max (state_machine.zig:58-81); 0 = 8190 */
+    uint64_t accounts_max;   /* capacity of the account store */
+    uint64_t transfers_max;  /* capacity of the transfer store */
+} tbg_config;
+
+#define TBG_OK 0
+#define TBG_E_INVALID (-1)   /* input_valid() would reject the request */
+#define TBG_E_CAPACITY (-2)  /* store capacity exceeded (no state changed) */
+#define TBG_E_DEVICE (-3)    /* HIP runtime / device failure: fatal */
+#define TBG_E_STATE (-4)     /* API misuse (e.g. commit timestamp not increasing) */
+
+/* StateMachine.init (state_machine.zig:455-477) / deinit (:479-484). */
+int tbg_create(const tbg_config *config, tbg_engine **out);
+int tbg_destroy(tbg_engine *engine);
+
+/* StateMachine.input_valid (state_machine.zig:543-572). Returns 1 valid, 0 invalid. */
+int tbg_input_valid(const tbg_engine *engine, uint32_t operation, uint64_t input_len);
+
+/* StateMachine.pulse (state_machine.zig:589-596): *needed = pulse_next_timestamp <= prepare_ts. */
+int tbg_pulse_needed(tbg_engine *engine, uint64_t prepare_timestamp, int *needed);
+
+/* StateMachine.prefetch (state_machine.zig:598-648): stages the request on the device and resolves
+ * account/transfer slots asynchronously. Optional: commit() prefetches itself if this was not
+ * called for the same input. */
+int tbg_prefetch(tbg_engine *engine, uint64_t op, uint32_t operation, const void *input, uint64_t input_len,
+                 uint64_t prefetch_timestamp);
+
+/* StateMachine.commit (state_machine.zig:1107-1146) for pulse, create_accounts, create_transfers,
+ * lookup_accounts and lookup_transfers. Writes exactly the reply bytes the reference writes into
+ * `output` (for create_*: packed {u32 index, u32 result} for non-ok events, ascending index) and
+ * the byte count into *output_len. Synchronous. */
+int tbg_commit(tbg_engine *engine, uint64_t op, uint64_t timestamp, uint32_t operation, const void *input,
+               uint64_t input_len, void *output, uint64_t output_cap, uint64_t *output_len);
+
+/* Device-resident streaming form of commit for create_transfers / create_accounts: events already
+ * in HBM, results left in HBM (d_results: n x 8 B; d_result_count: u32), fully asynchronous on the
+ * engine's stream. If `auto_pulse` is set, the pulse decision pulse_next <= prepare_timestamp and
+ * the pulse itself (at `timestamp`) run on the device before the batch, as the replica would. */
+int tbg_commit_device(tbg_engine *engine, uint32_t operation, uint64_t timestamp, const void *d_events, uint32_t n,
+                      void *d_results, uint32_t *d_result_count, int auto_pulse, uint64_t prepare_timestamp);
+
+/* Waits for all work queued on the engine's stream. */
+int tbg_sync(tbg_engine *engine);
+/* The engine's HIP stream (hipStream_t), for callers that time or order around it. */
+void *tbg_stream(tbg_engine *engine);
+
+/* Test hook mirroring the harness `setup` action (state_machine.zig:2545-2561). */
+int tbg_setup_balances(tbg_engine *engine, const tb_uint128_t *id, const tb_uint128_t *debits_pending,
+                       const tb_uint128_t *debits_posted, const tb_uint128_t *credits_pending,
+                       const tb_uint128_t *credits_posted);
+
+typedef struct tbg_stats {
+    uint64_t accounts;        /* accounts stored */
+    uint64_t transfers;       /* transfers stored */
+    uint64_t expiry_entries;  /* entries in the live expires_at list */
+    uint64_t pulse_next_timestamp;
+    uint64_t events_total;    /* create_* events committed through the engine */
+    uint64_t walker_events;   /* of which ran on the sequential walker */
+} tbg_stats;
+int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
+
+/* Whole-state dumps in creation (= timestamp) order, for parity checks. */
+int tbg_dump_accounts(tbg_engine *engine, tb_account_t *out, uint64_t cap, uint64_t *count);
+int tbg_dump_transfers(tbg_engine *engine, tb_transfer_t *out, uint64_t cap, uint64_t *count);
+/* Pending status per stored transfer (0 none, 1 pending, 2 posted, 3 voided, 4 expired). */
+int tbg_dump_transfer_status(tbg_engine *engine, uint8_t *out, uint64_t cap, uint64_t *count);
+/* Device pointers to the dense stores (for on-device digests); valid until the next commit. */
+int tbg_device_stores(tbg_engine *engine, const tb_account_t **accounts, const tb_transfer_t **transfers);
+
+/* Synthetic request streams generated directly in HBM (tigerbeetle_amd/csrc/workload.hip),
+ * shaped like the reference benchmark (src/tigerbeetle/benchmark_load.zig:206-327). `stream` is a
+ * hipStream_t (e.g. tbg_stream(engine)). Bit-identical to tigerbeetle_amd/workload.py. */
+int tbg_gen_accounts(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint32_t ledger, uint16_t code,
+                     uint16_t flags, void *stream);
+int tbg_gen_transfers_uniform(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
+                              uint64_t id_offset, void *stream);
+
+/* Introspection of the last create_* batch: per-event class bits and final codes (debugging). */
+int tbg_debug_last_batch(tbg_engine *engine, uint32_t *cls, uint32_t *code, uint32_t n);
+
+/* Library build identification ("gfx950 ..."). */
+const char *tbg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TBG_H */

@@ -1,0 +1,82 @@
+"""Loader for the in-tree HIP library (libtbgpu.so). The product path has no fallback: if the
+library is missing or cannot load, every entry point raises."""
+import ctypes
+import os
+
+from .types import ACCOUNT_DTYPE  # noqa: F401  (keeps the dtypes importable alongside the lib)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtbgpu.so")
+
+# Every symbol declared in include/tbg.h.
+EXPORTS = [
+    "tbg_create", "tbg_destroy", "tbg_input_valid", "tbg_pulse_needed", "tbg_prefetch", "tbg_commit",
+    "tbg_commit_device", "tbg_sync", "tbg_stream", "tbg_setup_balances", "tbg_get_stats",
+    "tbg_dump_accounts", "tbg_dump_transfers", "tbg_dump_transfer_status", "tbg_device_stores",
+    "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_version", "tbg_debug_last_batch",
+]
+
+
+class U128(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64)]
+
+
+def u128(v):
+    return U128(v & 0xFFFFFFFFFFFFFFFF, (v >> 64) & 0xFFFFFFFFFFFFFFFF)
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("batch_max", ctypes.c_uint32),
+                ("accounts_max", ctypes.c_uint64), ("transfers_max", ctypes.c_uint64)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("accounts", ctypes.c_uint64), ("transfers", ctypes.c_uint64),
+                ("expiry_entries", ctypes.c_uint64), ("pulse_next_timestamp", ctypes.c_uint64),
+                ("events_total", ctypes.c_uint64), ("walker_events", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+    P = ctypes.POINTER
+    sig = {
+        "tbg_create": ([P(Config), P(vp)], i32),
+        "tbg_destroy": ([vp], i32),
+        "tbg_input_valid": ([vp, u32, u64], i32),
+        "tbg_pulse_needed": ([vp, u64, P(ctypes.c_int)], i32),
+        "tbg_prefetch": ([vp, u64, u32, vp, u64, u64], i32),
+        "tbg_commit": ([vp, u64, u64, u32, vp, u64, vp, u64, P(u64)], i32),
+        "tbg_commit_device": ([vp, u32, u64, vp, u32, vp, vp, ctypes.c_int, u64], i32),
+        "tbg_sync": ([vp], i32),
+        "tbg_stream": ([vp], vp),
+        "tbg_setup_balances": ([vp, P(U128), P(U128), P(U128), P(U128), P(U128)], i32),
+        "tbg_get_stats": ([vp, P(Stats)], i32),
+        "tbg_dump_accounts": ([vp, vp, u64, P(u64)], i32),
+        "tbg_dump_transfers": ([vp, vp, u64, P(u64)], i32),
+        "tbg_dump_transfer_status": ([vp, vp, u64, P(u64)], i32),
+        "tbg_device_stores": ([vp, P(vp), P(vp)], i32),
+        "tbg_gen_accounts": ([vp, u64, u64, u64, u32, ctypes.c_uint16, ctypes.c_uint16, vp], i32),
+        "tbg_gen_transfers_uniform": ([vp, u64, u64, u64, u64, u64, vp], i32),
+        "tbg_version": ([], ctypes.c_char_p),
+        "tbg_debug_last_batch": ([vp, vp, vp, u32], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with status {rc}")

@@ -1,0 +1,199 @@
+// dev_common.h — device-side layout of the engine's HBM state and the shared primitives.
+//
+// HBM layout (one engine per GPU):
+//   acc_tab  AccEntry[acc_cap]   open-addressing id -> slot table, 32 B entries (id, slot, ledger,
+//                                flags): the transfer path resolves an account and checks ledger and
+//                                limit flags from this one line, never touching the 128 B record.
+//   acc      tb_account_t[]      dense Account records in creation (= timestamp) order.
+//   x_tab    XEntry[x_cap]       id -> slot table for transfers, 32 B entries.
+//   xr       tb_transfer_t[]     dense Transfer records in commit (= timestamp) order.
+//   xstatus  u8[]                TransferPending.status per transfer slot (0 = none). Keyed by slot
+//                                instead of by timestamp: slot order == timestamp order, 1:1.
+//   exp/alt  ExpEntry[]          live pending-with-timeout list (the `expires_at` index).
+// Capacities are powers of two with load factor <= 1/2.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tb_types.h"
+
+typedef unsigned __int128 u128;
+
+#define NONE32 0xFFFFFFFFu
+#define CONT 0xFFFFFFFFu  // "no result yet, keep evaluating"
+
+static constexpr u128 MAX128 = ~(u128)0;
+
+struct __attribute__((aligned(32))) AccEntry {
+  uint64_t id_lo, id_hi;
+  uint32_t slot;  // NONE32 = empty
+  uint32_t ledger;
+  uint16_t flags;
+  uint16_t pad0;
+  uint32_t pad1;
+};
+static_assert(sizeof(AccEntry) == 32, "AccEntry");
+
+struct __attribute__((aligned(32))) XEntry {
+  uint64_t id_lo, id_hi;
+  uint32_t slot;  // NONE32 = empty
+  uint32_t pad0;
+  uint64_t pad1;
+};
+static_assert(sizeof(XEntry) == 32, "XEntry");
+
+// Batch-local key map (one per batch, cleaned by the last kernel of the batch). Keys are never
+// stored: `owner` names the first event that claimed the entry, and bit 31 says whether the key is
+// that event's `id` or its `pending_id`; comparing against the immutable input events avoids any
+// reader/writer race on a 128-bit key.
+struct __attribute__((aligned(32))) BEntry {
+  uint32_t owner;      // NONE32 = empty
+  uint32_t id_count;   // events (reaching the exists check) with this id
+  uint32_t pid_count;  // post/void events with this pending_id
+  int32_t committed;   // walker: index of the in-batch event currently holding this id, -1 none
+  uint32_t pad[4];
+};
+static_assert(sizeof(BEntry) == 32, "BEntry");
+
+struct __attribute__((aligned(16))) ExpEntry {
+  uint64_t expires_at;
+  uint32_t slot;
+  uint32_t pad;
+};
+
+// Device-global scalars (one cache line each group).
+struct __attribute__((aligned(64))) Globals {
+  uint64_t acc_count;
+  uint64_t x_count;
+  uint64_t exp_count;
+  uint64_t pulse_next;  // ExpirePendingTransfers.pulse_next_timestamp (conservative)
+  u128 ovf_bound;       // >= every account's dp+dpo and cp+cpo (overflow-free batch test)
+  // per batch
+  u128 batch_amount_sum;
+  uint32_t batch_huge;
+  uint32_t epoch;
+  uint32_t result_count;
+  uint32_t insert_count;
+  uint32_t w_count;
+  uint32_t ovf_mode;
+  uint64_t base;  // acc_count / x_count at batch start (captured by the scan kernel)
+  // pulse
+  uint32_t cand_count;
+  uint32_t alt_count;
+  uint32_t expired_count;
+  uint32_t pad2;
+  uint64_t next_min;
+  // walker statistics (cumulative)
+  uint64_t w_events_total;
+  uint64_t events_total;
+};
+
+// Per-event class bits (scratch `cls`).
+enum : uint32_t {
+  C_STATIC = 1u << 0,      // code is final regardless of order/state (validation-stage result)
+  C_REACH = 1u << 1,       // reaches the exists check: id entered into the batch map
+  C_U = 1u << 2,           // order/state dependent: needs the sequential walker
+  C_W = 1u << 3,           // processed by the walker (U, touches a hot account, or chained with one)
+  C_LINKED = 1u << 4,
+  C_TSNZ = 1u << 5,        // event.timestamp != 0
+  C_INSERT = 1u << 6,      // static path: the event inserts its record if it executes (ok or quirk)
+  C_PENDING = 1u << 7,     // creates a pending transfer
+  C_POSTVOID = 1u << 8,
+  C_POST = 1u << 9,
+  C_READS_DR = 1u << 10,   // decision reads the debit account's balances
+  C_READS_CR = 1u << 11,
+  C_PV_PREBATCH = 1u << 12,// post/void whose pending transfer was found in the pre-batch table
+  C_COMMIT = 1u << 13,     // final: effects persist (set by the scan kernel)
+  C_INSERTED = 1u << 14,   // final: record inserted (ok, or the expired-post quirk)
+};
+
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+__host__ __device__ inline uint64_t hash_id(uint64_t lo, uint64_t hi) {
+  return mix64(lo ^ mix64(hi + 0x9e3779b97f4a7c15ull));
+}
+
+__device__ inline u128 U(const tb_uint128_t& v) { return ((u128)v.hi << 64) | v.lo; }
+__device__ inline tb_uint128_t W(u128 v) {
+  tb_uint128_t r;
+  r.lo = (uint64_t)v;
+  r.hi = (uint64_t)(v >> 64);
+  return r;
+}
+__device__ inline bool ovf128(u128 a, u128 b) { return a + b < a; }
+__device__ inline bool ovf64(uint64_t a, uint64_t b) { return a + b < a; }
+
+// 128-bit atomic add from two 64-bit atomics: the carry out of the low word is computed from the
+// value the low-word atomic returned, so concurrent adds compose to the exact 128-bit sum.
+__device__ inline void atomic_add_u128(tb_uint128_t* p, u128 v) {
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(p);
+  const unsigned long long lo = (unsigned long long)v, hi = (unsigned long long)(v >> 64);
+  const unsigned long long old = atomicAdd(w, lo);
+  const unsigned long long carry = (old + lo) < old ? 1ull : 0ull;
+  if (hi + carry) atomicAdd(w + 1, hi + carry);
+}
+__device__ inline void atomic_sub_u128(tb_uint128_t* p, u128 v) { atomic_add_u128(p, (u128)0 - v); }
+
+// ------------------------------------------------------------------------------------------------
+// Table probes (linear probing; thread-per-query; one 32 B entry per probe).
+// ------------------------------------------------------------------------------------------------
+__device__ inline uint32_t acc_find(const AccEntry* __restrict__ tab, uint64_t mask, tb_uint128_t id,
+                                    AccEntry* out) {
+  if ((id.lo | id.hi) == 0) return NONE32;
+  uint64_t h = hash_id(id.lo, id.hi) & mask;
+  for (;;) {
+    const AccEntry e = tab[h];
+    if (e.slot == NONE32) return NONE32;
+    if (e.id_lo == id.lo && e.id_hi == id.hi) {
+      *out = e;
+      return e.slot;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+__device__ inline uint32_t x_find(const XEntry* __restrict__ tab, uint64_t mask, tb_uint128_t id) {
+  if ((id.lo | id.hi) == 0) return NONE32;
+  uint64_t h = hash_id(id.lo, id.hi) & mask;
+  for (;;) {
+    const XEntry e = tab[h];
+    if (e.slot == NONE32) return NONE32;
+    if (e.id_lo == id.lo && e.id_hi == id.hi) return e.slot;
+    h = (h + 1) & mask;
+  }
+}
+
+// Inserts of distinct, absent keys: claim by CAS on the slot word, then publish the key. Readers
+// run in later kernels only.
+__device__ inline void acc_insert(AccEntry* tab, uint64_t mask, tb_uint128_t id, uint32_t slot, uint32_t ledger,
+                                  uint16_t flags) {
+  uint64_t h = hash_id(id.lo, id.hi) & mask;
+  for (;;) {
+    if (atomicCAS(&tab[h].slot, NONE32, slot) == NONE32) {
+      tab[h].id_lo = id.lo;
+      tab[h].id_hi = id.hi;
+      tab[h].ledger = ledger;
+      tab[h].flags = flags;
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+__device__ inline void x_insert(XEntry* tab, uint64_t mask, tb_uint128_t id, uint32_t slot) {
+  uint64_t h = hash_id(id.lo, id.hi) & mask;
+  for (;;) {
+    if (atomicCAS(&tab[h].slot, NONE32, slot) == NONE32) {
+      tab[h].id_lo = id.lo;
+      tab[h].id_hi = id.hi;
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}

@@ -1,0 +1,114 @@
+"""StateMachine boundary over the MI355X engine (libtbgpu.so).
+
+Mirrors the reference interface (src/state_machine.zig): `input_valid` (:543-572), `prepare`
+(:575-587), `pulse` (:589-596), `prefetch` (:598-648), `commit` (:1107-1146) and the public
+timestamp fields (:433-435), with the test-harness hook `setup_balances` (:2545-2561). Every call
+goes through the C ABI in include/tbg.h; there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .types import ACCOUNT_DTYPE, BATCH_MAX, TRANSFER_DTYPE, Operation
+
+MESSAGE_BODY_SIZE_MAX = 1048576 - 256
+
+
+class StateMachine:
+    def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20):
+        L = _lib.lib()
+        cfg = _lib.Config(device, batch_max, accounts_max, transfers_max)
+        h = ctypes.c_void_p()
+        _lib.check(L.tbg_create(ctypes.byref(cfg), ctypes.byref(h)), "tbg_create")
+        self.h = h
+        self.batch_max = batch_max
+        self.prepare_timestamp = 0
+        self.prefetch_timestamp = 0
+        self.commit_timestamp = 0
+        self._out = np.zeros(MESSAGE_BODY_SIZE_MAX, np.uint8)
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().tbg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def stream(self):
+        return _lib.lib().tbg_stream(self.h)
+
+    def input_valid(self, operation, data):
+        return bool(_lib.lib().tbg_input_valid(self.h, int(operation), len(data)))
+
+    def prepare(self, operation, data):
+        assert self.input_valid(operation, data)
+        if operation in (Operation.create_accounts, Operation.create_transfers):
+            self.prepare_timestamp += len(data) // 128
+
+    def pulse(self):
+        needed = ctypes.c_int()
+        _lib.check(_lib.lib().tbg_pulse_needed(self.h, self.prepare_timestamp, ctypes.byref(needed)), "pulse")
+        return bool(needed.value)
+
+    def prefetch(self, op, operation, data):
+        self._pf = np.frombuffer(data, np.uint8) if data else np.zeros(0, np.uint8)
+        ptr = self._pf.ctypes.data if len(data) else None
+        _lib.check(_lib.lib().tbg_prefetch(self.h, op, int(operation), ptr, len(data), self.prefetch_timestamp),
+                   "prefetch")
+
+    def commit(self, client, op, timestamp, operation, data):
+        buf = self._pf if getattr(self, "_pf", None) is not None and self._pf.tobytes() == data else (
+            np.frombuffer(data, np.uint8) if data else np.zeros(0, np.uint8))
+        ptr = buf.ctypes.data if len(data) else None
+        n = ctypes.c_uint64()
+        _lib.check(_lib.lib().tbg_commit(self.h, op, timestamp, int(operation), ptr, len(data),
+                                         self._out.ctypes.data, len(self._out), ctypes.byref(n)), "commit")
+        self._pf = None
+        if operation in (Operation.create_accounts, Operation.create_transfers):
+            self.commit_timestamp = timestamp
+        return self._out[: n.value].tobytes()
+
+    # ---- test hooks / introspection -----------------------------------------------------------
+    def setup_balances(self, ident, dp, dpo, cp, cpo):
+        args = [ctypes.byref(_lib.u128(v)) for v in (ident, dp, dpo, cp, cpo)]
+        _lib.check(_lib.lib().tbg_setup_balances(self.h, *args), "setup_balances")
+
+    def stats(self):
+        s = _lib.Stats()
+        _lib.check(_lib.lib().tbg_get_stats(self.h, ctypes.byref(s)), "stats")
+        return {f: getattr(s, f) for f, _ in _lib.Stats._fields_}
+
+    def pulse_next_timestamp(self):
+        return self.stats()["pulse_next_timestamp"]
+
+    def dump_accounts(self):
+        n0 = self.stats()["accounts"]
+        out = np.zeros(max(n0, 1), ACCOUNT_DTYPE)
+        n = ctypes.c_uint64()
+        _lib.check(_lib.lib().tbg_dump_accounts(self.h, out.ctypes.data, n0, ctypes.byref(n)), "dump")
+        return out[: n.value]
+
+    def dump_transfers(self):
+        n0 = self.stats()["transfers"]
+        out = np.zeros(max(n0, 1), TRANSFER_DTYPE)
+        n = ctypes.c_uint64()
+        _lib.check(_lib.lib().tbg_dump_transfers(self.h, out.ctypes.data, n0, ctypes.byref(n)), "dump")
+        return out[: n.value]
+
+    def dump_transfer_status(self):
+        n0 = self.stats()["transfers"]
+        out = np.zeros(max(n0, 1), np.uint8)
+        n = ctypes.c_uint64()
+        _lib.check(_lib.lib().tbg_dump_transfer_status(self.h, out.ctypes.data, n0, ctypes.byref(n)), "dump")
+        return out[: n.value]
+
+    # ---- device-resident streaming ------------------------------------------------------------
+    def commit_device(self, operation, timestamp, d_events, n, d_results, d_count, auto_pulse, prepare_timestamp):
+        _lib.check(_lib.lib().tbg_commit_device(self.h, int(operation), timestamp, d_events, n, d_results, d_count,
+                                                int(auto_pulse), prepare_timestamp), "commit_device")
+
+    def sync(self):
+        _lib.check(_lib.lib().tbg_sync(self.h), "sync")
