@@ -104,6 +104,12 @@ int tbg_gen_accounts(void *d_out, uint64_t first, uint64_t count, uint64_t seed,
 int tbg_gen_transfers_uniform(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
                               uint64_t id_offset, void *stream);
 
+/* Per-phase kernel timing with HIP events on the engine stream. Phases: 0 prep, 1 link, 2 mark,
+ * 3 scan+walk, 4 apply, 5 pulse (all five pulse kernels). collect() synchronizes, returns the summed
+ * milliseconds and launch counts per phase since the last collect, and resets. */
+int tbg_timing_enable(tbg_engine *engine, int enable);
+int tbg_timing_collect(tbg_engine *engine, double *ms, uint64_t *launches, uint32_t n_phases);
+
 /* Introspection of the last create_* batch: per-event class bits and final codes (debugging). */
 int tbg_debug_last_batch(tbg_engine *engine, uint32_t *cls, uint32_t *code, uint32_t n);
 

@@ -14,6 +14,7 @@ EXPORTS = [
     "tbg_commit_device", "tbg_sync", "tbg_stream", "tbg_setup_balances", "tbg_get_stats",
     "tbg_dump_accounts", "tbg_dump_transfers", "tbg_dump_transfer_status", "tbg_device_stores",
     "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_version", "tbg_debug_last_batch",
+    "tbg_timing_enable", "tbg_timing_collect",
 ]
 
 
@@ -68,6 +69,8 @@ def lib():
         "tbg_gen_transfers_uniform": ([vp, u64, u64, u64, u64, u64, vp], i32),
         "tbg_version": ([], ctypes.c_char_p),
         "tbg_debug_last_batch": ([vp, vp, vp, u32], i32),
+        "tbg_timing_enable": ([vp, ctypes.c_int], i32),
+        "tbg_timing_collect": ([vp, vp, vp, u32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -27,7 +27,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <new>
+
 #include <algorithm>
+#include <vector>
 
 #include "../../include/tbg.h"
 #include "dev_common.h"
@@ -205,6 +208,9 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
           pid_ent = bmap_claim(s.bmap, s.bmask, evb, t.pending_id, i | 0x80000000u);
           atomicAdd(&s.bmap[id_ent].id_count, 1u);
           atomicAdd(&s.bmap[pid_ent].pid_count, 1u);
+          // Resolved for every post/void that reaches the pending lookup: the walker needs it even
+          // when the pending transfer itself is created in this batch.
+          id_tslot = x_find(d.x_tab, d.x_mask, t.id);
           p_tslot = x_find(d.x_tab, d.x_mask, t.pending_id);
           if (p_tslot == NONE32) {
             code = TB_CT_PENDING_TRANSFER_NOT_FOUND;  // unless created in-batch (then U)
@@ -217,10 +223,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
               dr_slot = acc_find(d.acc_tab, d.acc_mask, p.debit_account_id, &de);
               cr_slot = acc_find(d.acc_tab, d.acc_mask, p.credit_account_id, &ce);
             }
-            if (code == CONT) {
-              id_tslot = x_find(d.x_tab, d.x_mask, t.id);
-              if (id_tslot != NONE32) code = pv_exists(t, d.xr[id_tslot], p);
-            }
+            if (code == CONT && id_tslot != NONE32) code = pv_exists(t, d.xr[id_tslot], p);
             if (code == CONT) code = pv_status(d.xstatus[p_tslot]);
             if (code == CONT) {
               cls |= C_INSERT;
@@ -1054,6 +1057,11 @@ struct tbg_engine {
   void* h_pinned;  // pinned staging for H2D/D2H
   uint64_t acc_upper, x_upper;  // host-side upper bounds of the store counts
   uint32_t epoch;
+  // optional per-phase timing (HIP events on the engine stream)
+  int timing;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used;
+  std::vector<uint32_t> ev_phase;  // phase of each (start, end) pair
   // prefetch bookkeeping
   int pf_valid;
   uint32_t pf_operation;
@@ -1083,6 +1091,8 @@ extern "C" const char* tbg_version(void) { return "tbgpu 0.1 gfx950 (create_acco
 extern "C" int tbg_create(const tbg_config* cfg, tbg_engine** out) {
   if (!cfg || !out) return TBG_E_STATE;
   tbg_engine* e = (tbg_engine*)calloc(1, sizeof(tbg_engine));
+  new (&e->ev_pool) std::vector<hipEvent_t>();
+  new (&e->ev_phase) std::vector<uint32_t>();
   e->device = cfg->device;
   e->batch_max = cfg->batch_max ? cfg->batch_max : TB_BATCH_MAX;
   if (e->batch_max > SCAN_CAP) {
@@ -1171,6 +1181,9 @@ extern "C" int tbg_destroy(tbg_engine* e) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->h_pinned) (void)hipHostFree(e->h_pinned);
+  for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+  e->ev_pool.~vector();
+  e->ev_phase.~vector();
   (void)hipStreamDestroy(e->stream);
   free(e);
   return TBG_OK;
@@ -1213,13 +1226,35 @@ extern "C" int tbg_pulse_needed(tbg_engine* e, uint64_t prepare_timestamp, int* 
   return TBG_OK;
 }
 
+enum { PH_PREP, PH_LINK, PH_MARK, PH_SCAN, PH_APPLY, PH_PULSE, PH_COUNT };
+
+static hipEvent_t timing_event(tbg_engine* e) {
+  if (e->ev_used == e->ev_pool.size()) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    e->ev_pool.push_back(ev);
+  }
+  return e->ev_pool[e->ev_used++];
+}
+static void phase_begin(tbg_engine* e, uint32_t phase) {
+  if (!e->timing) return;
+  e->ev_phase.push_back(phase);
+  (void)hipEventRecord(timing_event(e), e->stream);
+}
+static void phase_end(tbg_engine* e) {
+  if (!e->timing) return;
+  (void)hipEventRecord(timing_event(e), e->stream);
+}
+
 static int launch_pulse(tbg_engine* e, uint64_t T, uint64_t prepare_timestamp) {
   hipStream_t st = e->stream;
+  phase_begin(e, PH_PULSE);
   k_pulse_gate<<<1, 1, 0, st>>>(e->d, e->ctl, prepare_timestamp);
   k_pulse_scan<<<1024, 256, 0, st>>>(e->d, e->s, e->ctl, T);
   k_pulse_select<<<1, 1024, 0, st>>>(e->d, e->s, e->ctl, e->batch_max);
   k_pulse_apply<<<512, 256, 0, st>>>(e->d, e->s, e->ctl);
   k_pulse_finish<<<1, 1, 0, st>>>(e->d, e->ctl);
+  phase_end(e);
   HIPCHK(hipGetLastError());
   return TBG_OK;
 }
@@ -1239,10 +1274,12 @@ static int check_capacity(tbg_engine* e, uint32_t operation, uint32_t n) {
 
 static int launch_prep(tbg_engine* e, uint32_t operation, const void* d_events, uint32_t n, uint64_t T) {
   hipStream_t st = e->stream;
+  phase_begin(e, PH_PREP);
   if (operation == TB_OP_CREATE_TRANSFERS)
     k_ct_prep<<<grid_for(n), 256, 0, st>>>(e->d, e->s, (const tb_transfer_t*)d_events, n, T);
   else
     k_ca_prep<<<grid_for(n), 256, 0, st>>>(e->d, e->s, (const tb_account_t*)d_events, n);
+  phase_end(e);
   HIPCHK(hipGetLastError());
   return TBG_OK;
 }
@@ -1252,10 +1289,18 @@ static int launch_rest(tbg_engine* e, uint32_t operation, const void* d_events, 
   hipStream_t st = e->stream;
   const uint32_t epoch = ++e->epoch;
   if (operation == TB_OP_CREATE_TRANSFERS) {
+    phase_begin(e, PH_LINK);
     k_ct_link<<<grid_for(n), 256, 0, st>>>(e->d, e->s, n, epoch);
+    phase_end(e);
+    phase_begin(e, PH_MARK);
     k_ct_mark<<<grid_for(n), 256, 0, st>>>(e->d, e->s, n, epoch);
+    phase_end(e);
+    phase_begin(e, PH_SCAN);
     k_scan_walk<true><<<1, SCAN_THREADS, 0, st>>>(e->d, e->s, (const uint8_t*)d_events, n, T, d_results, d_count);
+    phase_end(e);
+    phase_begin(e, PH_APPLY);
     k_ct_apply<<<grid_for(n), 256, 0, st>>>(e->d, e->s, (const tb_transfer_t*)d_events, n, T);
+    phase_end(e);
     e->x_upper += n;
   } else {
     k_ca_link<<<grid_for(n), 256, 0, st>>>(e->s, n);
@@ -1441,6 +1486,35 @@ extern "C" int tbg_dump_transfer_status(tbg_engine* e, uint8_t* out, uint64_t ca
   int rc = read_globals(e, &g);
   if (rc) return rc;
   return dump(e, e->d.xstatus, 1, g.x_count, out, cap, count);
+}
+
+// Per-phase timing: when enabled, every kernel phase is bracketed by HIP events on the engine
+// stream. tbg_timing_collect() synchronizes, sums the elapsed times per phase (ms) and counts the
+// launches, then resets.
+extern "C" int tbg_timing_enable(tbg_engine* e, int enable) {
+  e->timing = enable;
+  return TBG_OK;
+}
+
+extern "C" int tbg_timing_collect(tbg_engine* e, double* ms, uint64_t* launches, uint32_t n_phases) {
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  for (uint32_t p = 0; p < n_phases; p++) {
+    ms[p] = 0;
+    launches[p] = 0;
+  }
+  for (size_t k = 0; k < e->ev_phase.size(); k++) {
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, e->ev_pool[2 * k], e->ev_pool[2 * k + 1]));
+    const uint32_t p = e->ev_phase[k];
+    if (p < n_phases) {
+      ms[p] += t;
+      launches[p]++;
+    }
+  }
+  e->ev_phase.clear();
+  e->ev_used = 0;
+  return TBG_OK;
 }
 
 // Debug/introspection: per-event class bits and codes of the last batch.
