@@ -30,6 +30,8 @@ typedef struct tbg_config {
     uint32_t batch_max;      /* constants.batch_max (state_machine.zig:58-81); 0 = 8190 */
     uint64_t accounts_max;   /* capacity of the account store */
     uint64_t transfers_max;  /* capacity of the transfer store */
+    uint32_t window_events_max; /* events per commit window (tbg_commit_window); 0 = batch_max */
+    uint32_t reserved;
 } tbg_config;
 
 #define TBG_OK 0
@@ -68,7 +70,20 @@ int tbg_commit(tbg_engine *engine, uint64_t op, uint64_t timestamp, uint32_t ope
 int tbg_commit_device(tbg_engine *engine, uint32_t operation, uint64_t timestamp, const void *d_events, uint32_t n,
                       void *d_results, uint32_t *d_result_count, int auto_pulse, uint64_t prepare_timestamp);
 
-/* Waits for all work queued on the engine's stream. */
+/* Super-batching: commits n_batches consecutive prepared batches (events contiguous in HBM at
+ * d_events, batch b has batch_events[b] events and commit timestamp batch_timestamps[b]) in one
+ * pass, with results identical to committing them one by one. Replies land in d_results,
+ * concatenated per batch: batch b's replies are entries [d_batch_base[b], d_batch_base[b+1]), each
+ * with a batch-relative index. Requires that no pulse can fall due between the window's batches
+ * (the device checks this; tbg_sync() then fails with TBG_E_STATE). With `auto_pulse`, the pulse
+ * decision for the first batch (pulse_next <= prepare_timestamp) and the pulse run first.
+ * Asynchronous on the engine stream. n_batches <= 64, total events <= window_events_max. */
+int tbg_commit_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_batches,
+                      const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_results,
+                      uint32_t *d_batch_base, int auto_pulse, uint64_t prepare_timestamp);
+
+/* Waits for all work queued on the engine's stream; TBG_E_STATE if a submitted window needed a
+ * pulse inside it (its results must not be trusted). */
 int tbg_sync(tbg_engine *engine);
 /* The engine's HIP stream (hipStream_t), for callers that time or order around it. */
 void *tbg_stream(tbg_engine *engine);
@@ -104,8 +119,8 @@ int tbg_gen_accounts(void *d_out, uint64_t first, uint64_t count, uint64_t seed,
 int tbg_gen_transfers_uniform(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
                               uint64_t id_offset, void *stream);
 
-/* Per-phase kernel timing with HIP events on the engine stream. Phases: 0 prep, 1 link, 2 mark,
- * 3 scan+walk, 4 apply, 5 pulse (all five pulse kernels). collect() synchronizes, returns the summed
+/* Per-phase kernel timing with HIP events on the engine stream. Phases: 0 prep, 1 link,
+ * 2 classify, 3 wcount, 4 wlist, 5 walk, 6 final, 7 pulse (all five pulse kernels). collect() synchronizes, returns the summed
  * milliseconds and launch counts per phase since the last collect, and resets. */
 int tbg_timing_enable(tbg_engine *engine, int enable);
 int tbg_timing_collect(tbg_engine *engine, double *ms, uint64_t *launches, uint32_t n_phases);

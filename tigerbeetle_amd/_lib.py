@@ -11,7 +11,7 @@ LIB_PATH = os.path.join(HERE, "libtbgpu.so")
 # Every symbol declared in include/tbg.h.
 EXPORTS = [
     "tbg_create", "tbg_destroy", "tbg_input_valid", "tbg_pulse_needed", "tbg_prefetch", "tbg_commit",
-    "tbg_commit_device", "tbg_sync", "tbg_stream", "tbg_setup_balances", "tbg_get_stats",
+    "tbg_commit_device", "tbg_commit_window", "tbg_sync", "tbg_stream", "tbg_setup_balances", "tbg_get_stats",
     "tbg_dump_accounts", "tbg_dump_transfers", "tbg_dump_transfer_status", "tbg_device_stores",
     "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_version", "tbg_debug_last_batch",
     "tbg_timing_enable", "tbg_timing_collect",
@@ -28,7 +28,8 @@ def u128(v):
 
 class Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("batch_max", ctypes.c_uint32),
-                ("accounts_max", ctypes.c_uint64), ("transfers_max", ctypes.c_uint64)]
+                ("accounts_max", ctypes.c_uint64), ("transfers_max", ctypes.c_uint64),
+                ("window_events_max", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class Stats(ctypes.Structure):
@@ -44,6 +45,13 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch ships its own libamdhip64 (same soname). Loading torch first
+    # makes libtbgpu bind to that copy; loading libtbgpu first and torch later would put two runtimes
+    # in the process and torch would see no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
     L = ctypes.CDLL(LIB_PATH)
@@ -57,6 +65,7 @@ def lib():
         "tbg_prefetch": ([vp, u64, u32, vp, u64, u64], i32),
         "tbg_commit": ([vp, u64, u64, u32, vp, u64, vp, u64, P(u64)], i32),
         "tbg_commit_device": ([vp, u32, u64, vp, u32, vp, vp, ctypes.c_int, u64], i32),
+        "tbg_commit_window": ([vp, u32, vp, u32, vp, vp, vp, vp, ctypes.c_int, u64], i32),
         "tbg_sync": ([vp], i32),
         "tbg_stream": ([vp], vp),
         "tbg_setup_balances": ([vp, P(U128), P(U128), P(U128), P(U128), P(U128)], i32),

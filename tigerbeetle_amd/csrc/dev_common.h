@@ -75,7 +75,7 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t result_count;
   uint32_t insert_count;
   uint32_t w_count;
-  uint32_t ovf_mode;
+  uint32_t window_error;  // a multi-batch window was submitted although a pulse could fall due inside
   uint64_t base;  // acc_count / x_count at batch start (captured by the scan kernel)
   // pulse
   uint32_t cand_count;

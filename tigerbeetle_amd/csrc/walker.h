@@ -1,0 +1,229 @@
+// walker.h — the sequential walker: the reference executor loop (state_machine.zig:1236-1301)
+// restricted to the window's W events, in window order, with an undo log standing in for
+// scope_open/scope_close (lsm/cache_map.zig:254-301). Everything else in the window is order-free
+// and already resolved in parallel; W carries exactly the events whose outcome depends on order.
+#pragma once
+#include "sm_logic.h"
+#include "window.h"
+
+// Batch-local key map helpers (keys are never stored; see BEntry).
+__device__ inline tb_uint128_t bkey(const uint8_t* ev, uint32_t owner) {
+  const uint32_t idx = owner & 0x7FFFFFFFu;
+  return *reinterpret_cast<const tb_uint128_t*>(ev + (size_t)idx * 128 + ((owner >> 31) ? 64 : 0));
+}
+
+__device__ inline uint32_t bmap_claim(BEntry* bm, uint32_t mask, const uint8_t* ev, tb_uint128_t key,
+                                      uint32_t owner) {
+  uint32_t h = (uint32_t)hash_id(key.lo, key.hi) & mask;
+  for (;;) {
+    const uint32_t old = atomicCAS(&bm[h].owner, NONE32, owner);
+    if (old == NONE32) return h;
+    const tb_uint128_t k = bkey(ev, old);
+    if (k.lo == key.lo && k.hi == key.hi) return h;
+    h = (h + 1) & mask;
+  }
+}
+
+__device__ inline void bmap_reset(BEntry* bm, uint32_t e) {
+  bm[e].owner = NONE32;
+  bm[e].id_count = 0;
+  bm[e].pid_count = 0;
+  bm[e].committed = -1;
+}
+
+struct Walker {
+  Dev d;
+  Scratch s;
+  const uint8_t* ev;
+  const WinDesc* w;
+  uint32_t undo_n;
+  bool scope;
+
+  __device__ void log_bal(uint32_t slot) {
+    if (!scope) return;
+    UndoRec& r = s.undo[undo_n++];
+    r.kind = UNDO_BAL;
+    r.a = slot;
+    const Bal b = load_bal(&d.acc[slot]);
+    r.old[0] = b.dp;
+    r.old[1] = b.dpo;
+    r.old[2] = b.cp;
+    r.old[3] = b.cpo;
+  }
+  __device__ void log_small(uint32_t kind, uint32_t a, u128 old) {
+    if (!scope) return;
+    UndoRec& r = s.undo[undo_n++];
+    r.kind = kind;
+    r.a = a;
+    r.old[0] = old;
+  }
+  __device__ void rollback() {
+    while (undo_n) {
+      const UndoRec& r = s.undo[--undo_n];
+      switch (r.kind) {
+        case UNDO_BAL: {
+          Bal b;
+          b.dp = r.old[0];
+          b.dpo = r.old[1];
+          b.cp = r.old[2];
+          b.cpo = r.old[3];
+          store_bal(&d.acc[r.a], b);
+        } break;
+        case UNDO_XST: d.xstatus[r.a] = (uint8_t)r.old[0]; break;
+        case UNDO_BST: s.bstatus[r.a] = (uint8_t)r.old[0]; break;
+        case UNDO_COMMIT: s.bmap[r.a].committed = (int32_t)(uint32_t)r.old[0]; break;
+        case UNDO_INS: s.ins[r.a] = 0; break;
+      }
+    }
+  }
+
+  __device__ void commit_record(uint32_t i, const tb_transfer_t& t2) {
+    s.t2[i] = t2;
+    log_small(UNDO_INS, i, 0);
+    s.ins[i] = 1;
+    const uint32_t e = s.id_ent[i];
+    log_small(UNDO_COMMIT, e, (uint32_t)s.bmap[e].committed);
+    s.bmap[e].committed = (int32_t)i;
+  }
+
+  // create_transfer (:1462-1585) from the exists check on; validation results come from k_ct_prep.
+  __device__ uint32_t transfer(uint32_t i, uint32_t cls) {
+    if (cls & C_STATIC) return s.code[i];
+    tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev)[i];
+    t.timestamp = win_ts(*w, s.batch[i], i);
+    if (cls & C_POSTVOID) return post_or_void(i, t);
+    if (s.id_tslot[i] != NONE32) return ct_exists(t, d.xr[s.id_tslot[i]]);
+    const int32_t c = s.bmap[s.id_ent[i]].committed;
+    if (c >= 0) return ct_exists(t, s.t2[c]);
+    const uint32_t drs = s.dr_slot[i], crs = s.cr_slot[i];
+    tb_account_t* dra = &d.acc[drs];
+    tb_account_t* cra = &d.acc[crs];
+    Bal dr = load_bal(dra), cr = load_bal(cra);
+    u128 amount;
+    const uint32_t r = ct_balances(t, dr, dra->flags, cr, cra->flags, &amount);
+    if (r != TB_CT_OK) return r;
+    t.amount = W(amount);
+    commit_record(i, t);
+    log_bal(drs);
+    log_bal(crs);
+    if (t.flags & TB_TRANSFER_PENDING) {
+      dr.dp += amount;
+      cr.cp += amount;
+      s.bstatus[i] = TB_PENDING_PENDING;
+    } else {
+      dr.dpo += amount;
+      cr.cpo += amount;
+    }
+    store_bal(dra, dr);
+    store_bal(cra, cr);
+    return TB_CT_OK;
+  }
+
+  // post_or_void_pending_transfer (:1608-1741) from the pending lookup on.
+  __device__ uint32_t post_or_void(uint32_t i, const tb_transfer_t& t) {
+    const uint32_t pslot = s.p_tslot[i];
+    int32_t pc = -1;
+    uint32_t drs, crs;
+    tb_transfer_t p;
+    if (pslot != NONE32) {
+      p = d.xr[pslot];
+      drs = s.dr_slot[i];
+      crs = s.cr_slot[i];
+    } else {
+      pc = s.bmap[s.pid_ent[i]].committed;
+      if (pc < 0) return TB_CT_PENDING_TRANSFER_NOT_FOUND;
+      p = s.t2[pc];
+      drs = s.dr_slot[pc];
+      crs = s.cr_slot[pc];
+    }
+    u128 amount;
+    uint32_t r = pv_against(t, p, &amount);
+    if (r != CONT) return r;
+    if (s.id_tslot[i] != NONE32) return pv_exists(t, d.xr[s.id_tslot[i]], p);
+    const int32_t c = s.bmap[s.id_ent[i]].committed;
+    if (c >= 0) return pv_exists(t, s.t2[c], p);
+    r = pv_status(pc >= 0 ? s.bstatus[pc] : d.xstatus[pslot]);
+    if (r != CONT) return r;
+    commit_record(i, pv_record(t, p, amount));
+    if (p.timeout > 0 && expires_at_of(p) <= t.timestamp) return TB_CT_PENDING_TRANSFER_EXPIRED;
+    const uint8_t st = (t.flags & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
+    if (pc >= 0) {
+      log_small(UNDO_BST, (uint32_t)pc, s.bstatus[pc]);
+      s.bstatus[pc] = st;
+    } else {
+      log_small(UNDO_XST, pslot, d.xstatus[pslot]);
+      d.xstatus[pslot] = st;
+    }
+    tb_account_t* dra = &d.acc[drs];
+    tb_account_t* cra = &d.acc[crs];
+    Bal dr = load_bal(dra), cr = load_bal(cra);
+    log_bal(drs);
+    log_bal(crs);
+    const u128 pa = U(p.amount);
+    dr.dp -= pa;
+    cr.cp -= pa;
+    if (t.flags & TB_TRANSFER_POST_PENDING) {
+      dr.dpo += amount;
+      cr.cpo += amount;
+    }
+    store_bal(dra, dr);
+    store_bal(cra, cr);
+    return TB_CT_OK;
+  }
+
+  // create_account (:1421-1448) from the exists check on.
+  __device__ uint32_t account(uint32_t i, uint32_t cls) {
+    if (cls & C_STATIC) return s.code[i];
+    if (s.id_tslot[i] != NONE32) return s.code[i];  // exists before the window: static
+    const tb_account_t* evs = reinterpret_cast<const tb_account_t*>(ev);
+    const uint32_t e = s.id_ent[i];
+    const int32_t c = s.bmap[e].committed;
+    if (c >= 0) return ca_exists(evs[i], evs[c]);
+    log_small(UNDO_INS, i, 0);
+    s.ins[i] = 1;
+    log_small(UNDO_COMMIT, e, (uint32_t)c);
+    s.bmap[e].committed = (int32_t)i;
+    return TB_CA_OK;
+  }
+
+  template <bool XFER>
+  __device__ void run(uint32_t w_count) {
+    int32_t chain = -1;
+    bool broken = false;
+    undo_n = 0;
+    scope = false;
+    for (uint32_t k = 0; k < w_count; k++) {
+      const uint32_t i = s.wlist[k];
+      const uint32_t cls = s.cls[i];
+      const bool linked = cls & C_LINKED;
+      const uint32_t b = s.batch[i];
+      uint32_t r;
+      if (linked && chain < 0) {
+        chain = (int32_t)i;
+        undo_n = 0;
+        scope = true;
+      }
+      if (linked && i == w->off[b + 1] - 1) {
+        r = TB_CT_LINKED_EVENT_CHAIN_OPEN;
+      } else if (broken) {
+        r = TB_CT_LINKED_EVENT_FAILED;
+      } else if (cls & C_TSNZ) {
+        r = TB_CT_TIMESTAMP_MUST_BE_ZERO;
+      } else {
+        r = XFER ? transfer(i, cls) : account(i, cls);
+      }
+      if (r != TB_CT_OK && chain >= 0 && !broken) {
+        broken = true;
+        rollback();
+        for (uint32_t j = (uint32_t)chain; j < i; j++) s.code[j] = TB_CT_LINKED_EVENT_FAILED;
+      }
+      s.code[i] = r;
+      if (chain >= 0 && (!linked || r == TB_CT_LINKED_EVENT_CHAIN_OPEN)) {
+        chain = -1;
+        broken = false;
+        scope = false;
+        undo_n = 0;
+      }
+    }
+  }
+};

@@ -1,0 +1,126 @@
+// window.h — a commit window: up to MAXB consecutive prepared batches processed by one pass of the
+// kernels (super-batching). Batches keep their own commit timestamp T_b (events stamped
+// T_b - n_b + j + 1, state_machine.zig:1253), their own chain structure (chains never cross a batch
+// end: the last linked event of a batch is linked_event_chain_open, :1247) and their own reply
+// (results are emitted per batch in ascending event order, :1289-1290).
+#pragma once
+#include "dev_common.h"
+
+#define MAXB 64
+#define SEG 1024          // events per segment (scan / count granularity)
+#define SEG_THREADS 256   // threads per segment block (4 consecutive events each)
+
+struct WinDesc {
+  uint32_t nb;             // batches in the window
+  uint32_t E;              // events in the window
+  uint32_t off[MAXB + 1];  // event offset of each batch; off[nb] = E
+  uint64_t T[MAXB];        // commit timestamp of each batch
+};
+
+__device__ inline uint32_t win_batch(const WinDesc& w, uint32_t i) {
+  uint32_t lo = 0, hi = w.nb - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (w.off[mid] <= i)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ inline uint64_t win_ts(const WinDesc& w, uint32_t b, uint32_t i) {
+  const uint32_t n = w.off[b + 1] - w.off[b];
+  return w.T[b] - n + (i - w.off[b]) + 1;
+}
+
+enum : uint32_t { UNDO_BAL = 1, UNDO_XST, UNDO_BST, UNDO_COMMIT, UNDO_INS };
+struct __attribute__((aligned(16))) UndoRec {
+  uint32_t kind, a, pad0, pad1;
+  u128 old[4];
+};
+
+struct Dev {
+  AccEntry* acc_tab;
+  uint64_t acc_mask;
+  tb_account_t* acc;
+  uint32_t* hot;  // per account slot: epoch of the last window that marked it hot
+  XEntry* x_tab;
+  uint64_t x_mask;
+  tb_transfer_t* xr;
+  uint8_t* xstatus;
+  ExpEntry* exp[2];
+  uint32_t* exp_cur;  // device word selecting the live expiry buffer
+  Globals* g;
+};
+
+struct Scratch {
+  uint32_t *code, *cls, *dr_slot, *cr_slot, *id_tslot, *p_tslot, *id_ent, *pid_ent, *wlist;
+  uint16_t* batch;
+  uint8_t *ins, *bstatus;
+  u128 *amt, *pamt;
+  tb_transfer_t* t2;
+  BEntry* bmap;
+  uint32_t bmask;
+  UndoRec* undo;
+  uint32_t *cnt_w, *cnt_bad, *cnt_ins;  // per segment
+  ExpEntry* cand;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Scan helpers (wave64 shuffles + one LDS word per wave).
+// ------------------------------------------------------------------------------------------------
+__device__ inline uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  return v;
+}
+
+__device__ inline uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Exclusive prefix over the threads of a block of `nwaves` waves; *total = block sum.
+template <int NWAVES>
+__device__ inline uint32_t block_excl(uint32_t v, uint32_t* lds, uint32_t* total) {
+  const uint32_t inc = wave_incl_scan(v);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 63) lds[wave] = inc;
+  __syncthreads();
+  uint32_t wp = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NWAVES; k++) {
+    const uint32_t x = lds[k];
+    if (k < wave) wp += x;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return wp + inc - v;
+}
+
+template <int NWAVES>
+__device__ inline uint32_t block_sum(uint32_t v, uint32_t* lds) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  uint32_t tot = 0;
+#pragma unroll
+  for (int k = 0; k < NWAVES; k++) tot += lds[k];
+  __syncthreads();
+  return tot;
+}
+
+// Sum of per-segment counts cnt[0..seg) (the segment's global exclusive offset).
+__device__ inline uint32_t seg_prefix(const uint32_t* cnt, uint32_t seg, uint32_t* lds) {
+  uint32_t v = 0;
+  for (uint32_t j = threadIdx.x; j < seg; j += SEG_THREADS) v += cnt[j];
+  return block_sum<SEG_THREADS / 64>(v, lds);
+}

@@ -16,9 +16,10 @@ MESSAGE_BODY_SIZE_MAX = 1048576 - 256
 
 
 class StateMachine:
-    def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20):
+    def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20,
+                 window_events_max=0):
         L = _lib.lib()
-        cfg = _lib.Config(device, batch_max, accounts_max, transfers_max)
+        cfg = _lib.Config(device, batch_max, accounts_max, transfers_max, window_events_max, 0)
         h = ctypes.c_void_p()
         _lib.check(L.tbg_create(ctypes.byref(cfg), ctypes.byref(h)), "tbg_create")
         self.h = h
@@ -109,6 +110,16 @@ class StateMachine:
     def commit_device(self, operation, timestamp, d_events, n, d_results, d_count, auto_pulse, prepare_timestamp):
         _lib.check(_lib.lib().tbg_commit_device(self.h, int(operation), timestamp, d_events, n, d_results, d_count,
                                                 int(auto_pulse), prepare_timestamp), "commit_device")
+
+    def commit_window(self, operation, d_events, batch_events, batch_timestamps, d_results, d_batch_base,
+                      auto_pulse, prepare_timestamp):
+        """Super-batched commit of consecutive batches (tbg_commit_window); asynchronous."""
+        nb = len(batch_events)
+        ev = (ctypes.c_uint32 * nb)(*batch_events)
+        ts = (ctypes.c_uint64 * nb)(*batch_timestamps)
+        _lib.check(_lib.lib().tbg_commit_window(self.h, int(operation), d_events, nb, ev, ts, d_results,
+                                                d_batch_base, int(auto_pulse), prepare_timestamp),
+                   "commit_window")
 
     def sync(self):
         _lib.check(_lib.lib().tbg_sync(self.h), "sync")
