@@ -42,18 +42,24 @@ struct __attribute__((aligned(32))) XEntry {
 };
 static_assert(sizeof(XEntry) == 32, "XEntry");
 
-// Batch-local key map (one per batch, cleaned by the last kernel of the batch). Keys are never
-// stored: `owner` names the first event that claimed the entry, and bit 31 says whether the key is
-// that event's `id` or its `pending_id`; comparing against the immutable input events avoids any
-// reader/writer race on a 128-bit key.
-struct __attribute__((aligned(32))) BEntry {
-  uint32_t owner;      // NONE32 = empty
-  uint32_t id_count;   // events (reaching the exists check) with this id
-  uint32_t pid_count;  // post/void events with this pending_id
-  int32_t committed;   // walker: index of the in-batch event currently holding this id, -1 none
-  uint32_t pad[4];
+// Window-local key map. Entries are epoch-tagged (the window number), so a stale entry from an
+// earlier window reads as empty and nothing is ever reset. Keys are never stored: `key` names the
+// first event that claimed the entry (bit 20 says whether the key is that event's id or its
+// pending_id), and claims compare against the immutable input events, so there is no
+// reader/writer race on a 128-bit key. One 64-bit CAS claims an entry and bumps its counts.
+//   key:    [63:32] epoch | [24:23] pid_count (sat. 3) | [22:21] id_count (sat. 3) | [20] pid | [19:0] owner
+//   commit: [63:32] epoch | [31:0] walker: index of the in-window event holding this id
+struct __attribute__((aligned(16))) BEntry {
+  unsigned long long key;
+  unsigned long long commit;
 };
-static_assert(sizeof(BEntry) == 32, "BEntry");
+static_assert(sizeof(BEntry) == 16, "BEntry");
+
+__host__ __device__ inline uint32_t bk_epoch(unsigned long long k) { return (uint32_t)(k >> 32); }
+__host__ __device__ inline uint32_t bk_owner(unsigned long long k) { return (uint32_t)k & 0xFFFFFu; }
+__host__ __device__ inline uint32_t bk_is_pid(unsigned long long k) { return ((uint32_t)k >> 20) & 1u; }
+__host__ __device__ inline uint32_t bk_idc(unsigned long long k) { return ((uint32_t)k >> 21) & 3u; }
+__host__ __device__ inline uint32_t bk_pidc(unsigned long long k) { return ((uint32_t)k >> 23) & 3u; }
 
 struct __attribute__((aligned(16))) ExpEntry {
   uint64_t expires_at;

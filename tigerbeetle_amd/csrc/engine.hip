@@ -1,16 +1,16 @@
 // engine.hip — MI355X batch-apply engine for the StateMachine commit path (libtbgpu.so).
 //
 // A commit window (window.h: 1..64 consecutive prepared batches, up to the configured event cap)
-// runs as seven launches on the engine's stream:
+// runs as six launches on the engine's stream:
 //
 //   k_*_prep     grid   stateless validation (state_machine.zig:1424-1439, 1465-1489, 1614-1624),
 //                       account resolution through 32 B account-table entries (id, slot, ledger,
 //                       flags), pre-window transfer id / pending_id resolution, static post/void
-//                       evaluation (:1626-1696); every id / pending_id enters a window-local key map.
-//   k_*_link     grid   order-dependence ("U"): duplicate ids, in-window pending targets, contended
-//                       pending transfers, balance-reading decisions (limit flags, balancing, or any
-//                       overflow risk); accounts read by U events become hot.
-//   k_classify   grid   walker set W = U + events touching a hot account, closed over linked chains
+//                       evaluation (:1626-1696); every id / pending_id enters a window-local key map;
+//                       accounts read by balance-dependent decisions (limits, balancing) become hot.
+//   k_classify   grid   order-dependence ("U": duplicate ids, in-window pending targets, contended
+//                       pending transfers, balance reads, any overflow risk) and the walker set
+//                       W = U + events touching a hot account, closed over linked chains
 //                       (one thread per chain head); all other events get their final outcome here,
 //                       including whole static chains (first failure + linked_event_failed fill).
 //   k_wcount     grid   per-segment counts (W, failures, inserts).
@@ -36,11 +36,6 @@
 #include "sm_logic.h"
 #include "walker.h"
 #include "window.h"
-
-__global__ void k_bmap_init(BEntry* bm, uint32_t cap) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < cap) bmap_reset(bm, i);
-}
 
 // Probe continuation after a first entry was already loaded (lets the first probes of several
 // independent lookups be in flight together).
@@ -78,7 +73,8 @@ __device__ inline void check_window(const WinDesc& w, Globals* g) {
 // ------------------------------------------------------------------------------------------------
 // create_transfers: prep
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w) {
+__global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
+                                                 uint32_t epoch) {
   __shared__ u128 red[256];
   __shared__ uint32_t huge_any;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -114,10 +110,8 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
           const uint64_t hx = hash_id(t.id.lo, t.id.hi) & d.x_mask;
           const uint64_t hp = hash_id(t.pending_id.lo, t.pending_id.hi) & d.x_mask;
           const XEntry ex = d.x_tab[hx], ep = d.x_tab[hp];
-          id_ent = bmap_claim(s.bmap, s.bmask, evb, t.id, i);
-          pid_ent = bmap_claim(s.bmap, s.bmask, evb, t.pending_id, i | 0x80000000u);
-          atomicAdd(&s.bmap[id_ent].id_count, 1u);
-          atomicAdd(&s.bmap[pid_ent].pid_count, 1u);
+          id_ent = bmap_claim(s.bmap, s.bmask, evb, t.id, i, 0, epoch);
+          pid_ent = bmap_claim(s.bmap, s.bmask, evb, t.pending_id, i, 1, epoch);
           id_tslot = x_probe_from(d.x_tab, d.x_mask, hx, ex, t.id);
           p_tslot = x_probe_from(d.x_tab, d.x_mask, hp, ep, t.pending_id);
           if (p_tslot == NONE32) {
@@ -167,8 +161,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
             cls |= C_STATIC;
           } else {
             cls |= C_REACH;
-            id_ent = bmap_claim(s.bmap, s.bmask, evb, t.id, i);
-            atomicAdd(&s.bmap[id_ent].id_count, 1u);
+            id_ent = bmap_claim(s.bmap, s.bmask, evb, t.id, i, 0, epoch);
             const bool bal = f & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT);
             amount_upper = U(t.amount);
             if (bal && amount_upper == 0) amount_upper = (u128)0xFFFFFFFFFFFFFFFFull;
@@ -177,12 +170,18 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
               code = ct_exists(t, d.xr[id_tslot]);
             } else {
               if (f & TB_TRANSFER_PENDING) cls |= C_PENDING;
-              if ((de.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) || (f & TB_TRANSFER_BALANCING_DEBIT))
+              // A balance-reading decision makes the read account hot for this window (every event
+              // touching it then runs on the walker, in order).
+              if ((de.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) || (f & TB_TRANSFER_BALANCING_DEBIT)) {
                 cls |= C_READS_DR;
-              if ((ce.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) || (f & TB_TRANSFER_BALANCING_CREDIT))
+                d.hot[dr_slot] = epoch;
+              }
+              if ((ce.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) || (f & TB_TRANSFER_BALANCING_CREDIT)) {
                 cls |= C_READS_CR;
+                d.hot[cr_slot] = epoch;
+              }
               amt = U(t.amount);
-              // Overflow checks cannot fail in an overflow-free window (checked in k_ct_link).
+              // Overflow checks cannot fail in an overflow-free window (checked in k_classify).
               if (ovf64(t.timestamp, (uint64_t)t.timeout * TB_NS_PER_S)) {
                 code = TB_CT_OVERFLOWS_TIMEOUT;
               } else {
@@ -229,32 +228,11 @@ __device__ inline bool window_ovf_mode(const Globals* g) {
   return ovf128(g->ovf_bound, g->batch_amount_sum);
 }
 
-__global__ void __launch_bounds__(256) k_ct_link(Dev d, Scratch s, uint32_t E, uint32_t epoch) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E) return;
-  const uint32_t cls = s.cls[i];
-  if (!(cls & C_REACH)) return;
-  const bool ovf_mode = window_ovf_mode(d.g);
-  bool u = ovf_mode || (cls & (C_READS_DR | C_READS_CR));
-  const BEntry& e = s.bmap[s.id_ent[i]];
-  if (e.id_count > 1 || e.pid_count > 0) u = true;  // duplicate id, or a post/void targets this id
-  if (cls & C_POSTVOID) {
-    const BEntry& pe = s.bmap[s.pid_ent[i]];
-    if (pe.id_count > 0 || pe.pid_count > 1) u = true;  // pending created in-window, or contended
-  }
-  if (u) {
-    s.cls[i] = cls | C_U;
-    if (!ovf_mode) {
-      if (cls & C_READS_DR) d.hot[s.dr_slot[i]] = epoch;
-      if (cls & C_READS_CR) d.hot[s.cr_slot[i]] = epoch;
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
-// create_accounts: prep / link
+// create_accounts: prep
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_ca_prep(Dev d, Scratch s, const tb_account_t* __restrict__ ev, WinDesc w) {
+__global__ void __launch_bounds__(256) k_ca_prep(Dev d, Scratch s, const tb_account_t* __restrict__ ev, WinDesc w,
+                                                 uint32_t epoch) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) check_window(w, d.g);
   if (i >= w.E) return;
@@ -271,8 +249,7 @@ __global__ void __launch_bounds__(256) k_ca_prep(Dev d, Scratch s, const tb_acco
       cls |= C_STATIC;
     } else {
       cls |= C_REACH;
-      id_ent = bmap_claim(s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), a.id, i);
-      atomicAdd(&s.bmap[id_ent].id_count, 1u);
+      id_ent = bmap_claim(s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), a.id, i, 0, epoch);
       AccEntry e;
       slot = acc_find(d.acc_tab, d.acc_mask, a.id, &e);
       if (slot != NONE32) {
@@ -294,20 +271,34 @@ __global__ void __launch_bounds__(256) k_ca_prep(Dev d, Scratch s, const tb_acco
   s.ins[i] = 0;
 }
 
-__global__ void __launch_bounds__(256) k_ca_link(Scratch s, uint32_t E) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E) return;
-  const uint32_t cls = s.cls[i];
-  if ((cls & C_REACH) && s.bmap[s.id_ent[i]].id_count > 1) s.cls[i] = cls | C_U;
-}
-
 // ------------------------------------------------------------------------------------------------
 // classify: W closure over chains + final outcome of every non-W event.
 // ------------------------------------------------------------------------------------------------
+// U: the event's outcome depends on order or state.
 template <bool XFER>
-__device__ inline bool is_w(const Dev& d, const Scratch& s, uint32_t j, uint32_t cls, uint32_t epoch) {
-  if (cls & C_U) return true;
-  if (!XFER || !(cls & C_REACH)) return false;
+__device__ inline bool is_u(const Scratch& s, uint32_t j, uint32_t cls, uint32_t epoch, bool ovf_mode) {
+  if (!(cls & C_REACH)) return false;
+  const uint32_t e = s.id_ent[j];
+  if (!XFER) return bmap_idc(s.bmap, e, epoch) > 1;  // duplicate account id in the window
+  if (ovf_mode || (cls & (C_READS_DR | C_READS_CR))) return true;
+  // duplicate transfer id, or a post/void in the window targets this id
+  if (bmap_idc(s.bmap, e, epoch) > 1 || bmap_pidc(s.bmap, e, epoch) > 0) return true;
+  if (cls & C_POSTVOID) {
+    // pending transfer created in the window, or several post/voids of one pending transfer
+    const uint32_t pe = s.pid_ent[j];
+    if (bmap_idc(s.bmap, pe, epoch) > 0 || bmap_pidc(s.bmap, pe, epoch) > 1) return true;
+  }
+  return false;
+}
+
+// W: runs on the walker (U, or touches an account some U event reads).
+template <bool XFER>
+__device__ inline bool is_w(const Dev& d, const Scratch& s, uint32_t j, uint32_t* cls, uint32_t epoch, bool ovf_mode) {
+  if (is_u<XFER>(s, j, *cls, epoch, ovf_mode)) {
+    *cls |= C_U;
+    return true;
+  }
+  if (!XFER || !(*cls & C_REACH)) return false;
   const uint32_t dr = s.dr_slot[j], cr = s.cr_slot[j];
   return (dr != NONE32 && d.hot[dr] == epoch) || (cr != NONE32 && d.hot[cr] == epoch);
 }
@@ -316,14 +307,15 @@ template <bool XFER>
 __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, uint32_t epoch) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w.E) return;
+  const bool ovf_mode = XFER && window_ovf_mode(d.g);
   const uint32_t b = s.batch[i];
   const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
-  const uint32_t cls = s.cls[i];
+  uint32_t cls = s.cls[i];
   const bool linked = cls & C_LINKED;
   if (i != first && (s.cls[i - 1] & C_LINKED)) return;  // chain member: its head decides
   if (!linked) {
     // singleton (:1255-1259, :1289-1290)
-    if (is_w<XFER>(d, s, i, cls, epoch)) {
+    if (is_w<XFER>(d, s, i, &cls, epoch, ovf_mode)) {
       s.cls[i] = cls | C_W;
     } else {
       const uint32_t code = s.code[i];
@@ -336,8 +328,8 @@ __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, u
   bool any_w = false;
   uint32_t f = NONE32;
   for (uint32_t j = i;; j++) {
-    const uint32_t cj = j == i ? cls : s.cls[j];
-    if (is_w<XFER>(d, s, j, cj, epoch)) any_w = true;
+    uint32_t cj = s.cls[j];
+    if (is_w<XFER>(d, s, j, &cj, epoch, ovf_mode)) any_w = true;
     const bool lj = cj & C_LINKED;
     const uint32_t code = (lj && j == last) ? (uint32_t)TB_CT_LINKED_EVENT_CHAIN_OPEN : s.code[j];
     if (code != TB_CT_OK && f == NONE32) f = j;
@@ -362,26 +354,24 @@ __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, u
 }
 
 // ------------------------------------------------------------------------------------------------
-// Segment counts and the ordered W list.
+// Segment counts and the ordered W list (one event per thread, one 1024-event segment per block).
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(SEG_THREADS) k_wcount(Scratch s, uint32_t E) {
-  __shared__ uint32_t lds[SEG_THREADS / 64];
-  const uint32_t base = blockIdx.x * SEG + threadIdx.x * 4;
+__global__ void __launch_bounds__(SEG) k_wcount(Scratch s, uint32_t E) {
+  __shared__ uint32_t lds[SEG / 64];
+  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
   uint32_t nw = 0, nbad = 0, nins = 0;
-  for (int k = 0; k < 4; k++) {
-    const uint32_t i = base + k;
-    if (i >= E) break;
+  if (i < E) {
     const uint32_t cls = s.cls[i];
     if (cls & C_W) {
-      nw++;
+      nw = 1;
     } else {
-      nbad += s.code[i] != TB_CT_OK;
-      nins += (cls & C_INSERTED) ? 1u : 0u;
+      nbad = s.code[i] != TB_CT_OK;
+      nins = (cls & C_INSERTED) ? 1u : 0u;
     }
   }
-  nw = block_sum<SEG_THREADS / 64>(nw, lds);
-  nbad = block_sum<SEG_THREADS / 64>(nbad, lds);
-  nins = block_sum<SEG_THREADS / 64>(nins, lds);
+  nw = block_sum<SEG / 64>(nw, lds);
+  nbad = block_sum<SEG / 64>(nbad, lds);
+  nins = block_sum<SEG / 64>(nins, lds);
   if (threadIdx.x == 0) {
     s.cnt_w[blockIdx.x] = nw;
     s.cnt_bad[blockIdx.x] = nbad;
@@ -389,23 +379,15 @@ __global__ void __launch_bounds__(SEG_THREADS) k_wcount(Scratch s, uint32_t E) {
   }
 }
 
-__global__ void __launch_bounds__(SEG_THREADS) k_wlist(Scratch s, uint32_t E) {
-  __shared__ uint32_t lds[SEG_THREADS / 64];
+__global__ void __launch_bounds__(SEG) k_wlist(Scratch s, uint32_t E) {
+  __shared__ uint32_t lds[SEG / 64];
   if (s.cnt_w[blockIdx.x] == 0) return;  // uniform per block
-  const uint32_t prefix = seg_prefix(s.cnt_w, blockIdx.x, lds);
-  const uint32_t base = blockIdx.x * SEG + threadIdx.x * 4;
-  uint32_t flags = 0, n = 0;
-  for (int k = 0; k < 4; k++) {
-    const uint32_t i = base + k;
-    if (i < E && (s.cls[i] & C_W)) {
-      flags |= 1u << k;
-      n++;
-    }
-  }
+  const uint32_t prefix = seg_prefix<SEG>(s.cnt_w, blockIdx.x, lds);
+  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
+  const uint32_t w = (i < E && (s.cls[i] & C_W)) ? 1u : 0u;
   uint32_t tot;
-  uint32_t pos = prefix + block_excl<SEG_THREADS / 64>(n, lds, &tot);
-  for (int k = 0; k < 4; k++)
-    if (flags & (1u << k)) s.wlist[pos++] = base + k;
+  const uint32_t pos = prefix + block_excl<SEG / 64>(w, lds, &tot);
+  if (w) s.wlist[pos] = i;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -416,7 +398,7 @@ __global__ void __launch_bounds__(SEG_THREADS) k_wlist(Scratch s, uint32_t E) {
 
 template <bool XFER>
 __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const uint8_t* ev, WinDesc w,
-                                                        uint32_t nseg) {
+                                                        uint32_t nseg, uint32_t epoch) {
   __shared__ uint32_t lds[WALK_THREADS / 64];
   __shared__ uint32_t sbad[MAX_SEGS], sins[MAX_SEGS];
   if (threadIdx.x == 0) d.g->base = XFER ? d.g->x_count : d.g->acc_count;
@@ -433,6 +415,7 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
     wk.s = s;
     wk.ev = ev;
     wk.w = &w;
+    wk.epoch = epoch;
     wk.template run<XFER>(w_count);
     d.g->w_events_total += w_count;
     d.g->events_total += w.E;
@@ -456,7 +439,7 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
 }
 
 // ------------------------------------------------------------------------------------------------
-// final: ordered replies + insert ranks + effects (per segment block, 4 consecutive events/thread)
+// final: ordered replies + insert ranks + effects (one event per thread, one segment per block)
 // ------------------------------------------------------------------------------------------------
 struct FinalOut {
   tb_create_result_t* results;  // window replies, concatenated per batch
@@ -464,137 +447,142 @@ struct FinalOut {
   uint32_t* out_count;          // optional: total failures (single-batch callers)
 };
 
-__device__ inline void write_batch_bases(const WinDesc& w, uint32_t i, uint32_t b, uint32_t rank, FinalOut o) {
-  // event i opens batch b and every empty batch just before it
-  if (i != w.off[b]) return;
-  for (int32_t bb = (int32_t)b; bb >= 0 && w.off[bb] == i; bb--) o.batch_base[bb] = rank;
-}
+// A 128-bit atomic add split in two phases so that several can be in flight before any carry is
+// resolved: issue() adds the low word (returning the old value); finish() adds the high word plus
+// the carry out of the low word. Concurrent adds compose to the exact 128-bit sum.
+struct Add128 {
+  unsigned long long* hi;
+  unsigned long long lo_add, hi_add, old;
+  __device__ void issue(tb_uint128_t* p, u128 v) {
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(p);
+    hi = w + 1;
+    lo_add = (unsigned long long)v;
+    hi_add = (unsigned long long)(v >> 64);
+    old = atomicAdd(w, lo_add);
+  }
+  __device__ void finish() const {
+    const unsigned long long carry = (old + lo_add) < old ? 1ull : 0ull;
+    if (hi_add + carry) atomicAdd(hi, hi_add + carry);
+  }
+};
 
 template <bool XFER>
-__global__ void __launch_bounds__(SEG_THREADS) k_final(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w,
-                                                       FinalOut o) {
-  __shared__ uint32_t lds[SEG_THREADS / 64];
+__global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w, FinalOut o) {
+  __shared__ uint32_t lds[SEG / 64];
   const uint32_t E = w.E;
-  const uint32_t base = blockIdx.x * SEG + threadIdx.x * 4;
-  uint32_t cls4[4], code4[4];
-  uint32_t nbad = 0, nins = 0;
-  for (int k = 0; k < 4; k++) {
-    const uint32_t i = base + k;
-    cls4[k] = 0;
-    code4[k] = TB_CT_OK;
-    if (i >= E) continue;
-    cls4[k] = s.cls[i];
-    code4[k] = s.code[i];
-    nbad += code4[k] != TB_CT_OK;
-    const bool ins = (cls4[k] & C_W) ? s.ins[i] != 0 : (cls4[k] & C_INSERTED) != 0;
-    if (ins)
-      cls4[k] |= C_INSERTED;
-    else
-      cls4[k] &= ~C_INSERTED;
-    nins += ins;
+  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
+  uint32_t cls = 0, code = TB_CT_OK;
+  bool ins = false;
+  if (i < E) {
+    cls = s.cls[i];
+    code = s.code[i];
+    ins = (cls & C_W) ? s.ins[i] != 0 : (cls & C_INSERTED) != 0;
   }
-  const uint32_t pbad = seg_prefix(s.cnt_bad, blockIdx.x, lds);
-  const uint32_t pins = seg_prefix(s.cnt_ins, blockIdx.x, lds);
-  uint32_t tot;
-  uint32_t rbad = pbad + block_excl<SEG_THREADS / 64>(nbad, lds, &tot);
-  uint32_t rins = pins + block_excl<SEG_THREADS / 64>(nins, lds, &tot);
-  const Globals* g = d.g;
-  const uint64_t xbase = g->base;
-  for (int k = 0; k < 4; k++) {
-    const uint32_t i = base + k;
-    if (i >= E) break;
-    const uint32_t cls = cls4[k], code = code4[k];
-    const uint32_t b = s.batch[i];
-    write_batch_bases(w, i, b, rbad, o);
-    if (code != TB_CT_OK) {
-      tb_create_result_t r;
-      r.index = i - w.off[b];
-      r.result = code;
-      o.results[rbad++] = r;
-    }
-    const bool wev = cls & C_W;
-    if (XFER) {
-      const tb_transfer_t* ev = reinterpret_cast<const tb_transfer_t*>(ev_bytes);
-      if (cls & C_INSERTED) {
-        const uint64_t slot = xbase + rins++;
-        tb_transfer_t t2;
-        if (wev) {
-          t2 = s.t2[i];
-        } else {
-          t2 = ev[i];
-          t2.timestamp = win_ts(w, b, i);
-          if (cls & C_POSTVOID) t2 = pv_record(t2, d.xr[s.p_tslot[i]], s.amt[i]);
+  const uint32_t bad = code != TB_CT_OK;
+  const uint32_t pbad = seg_prefix<SEG>(s.cnt_bad, blockIdx.x, lds);
+  const uint32_t pins = seg_prefix<SEG>(s.cnt_ins, blockIdx.x, lds);
+  uint32_t tot_bad, tot_ins;
+  const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
+  const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
+  if (i >= E) return;
+  const uint64_t xbase = d.g->base;
+  const uint32_t b = s.batch[i];
+  if (i == w.off[b]) {
+    // event i opens batch b and every empty batch just before it
+    for (int32_t bb = (int32_t)b; bb >= 0 && w.off[bb] == i; bb--) o.batch_base[bb] = rbad;
+  }
+  if (bad) {
+    tb_create_result_t r;
+    r.index = i - w.off[b];
+    r.result = code;
+    o.results[rbad] = r;
+  }
+  const bool wev = cls & C_W;
+  if (XFER) {
+    const tb_transfer_t* ev = reinterpret_cast<const tb_transfer_t*>(ev_bytes);
+    // Balance deltas of non-W commits: low-word atomics issued first, carries resolved after the
+    // record and table writes below.
+    Add128 adds[4];
+    int nadd = 0;
+    if (!wev && (cls & C_COMMIT)) {
+      tb_account_t* dra = &d.acc[s.dr_slot[i]];
+      tb_account_t* cra = &d.acc[s.cr_slot[i]];
+      const u128 a = s.amt[i];
+      if (cls & C_POSTVOID) {
+        const u128 pa = s.pamt[i];
+        adds[nadd++].issue(&dra->debits_pending, (u128)0 - pa);
+        adds[nadd++].issue(&cra->credits_pending, (u128)0 - pa);
+        if (cls & C_POST) {
+          adds[nadd++].issue(&dra->debits_posted, a);
+          adds[nadd++].issue(&cra->credits_posted, a);
         }
-        d.xr[slot] = t2;
-        x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
-        uint8_t st = 0;
-        if (t2.flags & TB_TRANSFER_PENDING) {
-          st = wev ? s.bstatus[i] : (uint8_t)TB_PENDING_PENDING;
-          if (t2.timeout > 0) {
-            const uint64_t expires_at = expires_at_of(t2);
-            atomicMin(reinterpret_cast<unsigned long long*>(&d.g->pulse_next), (unsigned long long)expires_at);
-            const bool visible = !(t2.timestamp >> 63) && expires_at <= TB_TIMESTAMP_MAX;
-            if (st == TB_PENDING_PENDING && visible) {
-              const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), 1ull);
-              ExpEntry e;
-              e.expires_at = expires_at;
-              e.slot = (uint32_t)slot;
-              e.pad = 0;
-              d.exp[*d.exp_cur][q] = e;
-            }
-          }
-        }
-        d.xstatus[slot] = st;
-      }
-      if (!wev && (cls & C_COMMIT)) {
-        tb_account_t* dra = &d.acc[s.dr_slot[i]];
-        tb_account_t* cra = &d.acc[s.cr_slot[i]];
-        const u128 a = s.amt[i];
-        if (cls & C_POSTVOID) {
-          const u128 pa = s.pamt[i];
-          atomic_sub_u128(&dra->debits_pending, pa);
-          atomic_sub_u128(&cra->credits_pending, pa);
-          if (cls & C_POST) {
-            atomic_add_u128(&dra->debits_posted, a);
-            atomic_add_u128(&cra->credits_posted, a);
-          }
-          d.xstatus[s.p_tslot[i]] = (cls & C_POST) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
-        } else if (cls & C_PENDING) {
-          atomic_add_u128(&dra->debits_pending, a);
-          atomic_add_u128(&cra->credits_pending, a);
-        } else {
-          atomic_add_u128(&dra->debits_posted, a);
-          atomic_add_u128(&cra->credits_posted, a);
-        }
-      }
-      if (s.pid_ent[i] != NONE32) bmap_reset(s.bmap, s.pid_ent[i]);
-    } else {
-      const tb_account_t* ev = reinterpret_cast<const tb_account_t*>(ev_bytes);
-      if (cls & C_INSERTED) {
-        const uint64_t slot = xbase + rins++;
-        tb_account_t a = ev[i];
-        a.timestamp = win_ts(w, b, i);
-        d.acc[slot] = a;
-        d.hot[slot] = 0;
-        acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
-      }
-    }
-    if (s.id_ent[i] != NONE32) bmap_reset(s.bmap, s.id_ent[i]);
-    if (i == E - 1) {
-      // the window's last event: totals and window-level state
-      for (int32_t bb = (int32_t)w.nb; bb >= 0 && w.off[bb] == E; bb--) o.batch_base[bb] = rbad;
-      if (o.out_count) *o.out_count = rbad;
-      Globals* gw = d.g;
-      gw->result_count = rbad;
-      if (XFER) {
-        gw->x_count = xbase + rins;
-        const u128 sum = gw->ovf_bound + gw->batch_amount_sum;
-        gw->ovf_bound = (gw->batch_huge || sum < gw->ovf_bound) ? MAX128 : sum;
-        gw->batch_amount_sum = 0;
-        gw->batch_huge = 0;
+        d.xstatus[s.p_tslot[i]] = (cls & C_POST) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
+      } else if (cls & C_PENDING) {
+        adds[nadd++].issue(&dra->debits_pending, a);
+        adds[nadd++].issue(&cra->credits_pending, a);
       } else {
-        gw->acc_count = xbase + rins;
+        adds[nadd++].issue(&dra->debits_posted, a);
+        adds[nadd++].issue(&cra->credits_posted, a);
       }
+    }
+    if (ins) {
+      const uint64_t slot = xbase + rins;
+      tb_transfer_t t2;
+      if (wev) {
+        t2 = s.t2[i];
+      } else {
+        t2 = ev[i];
+        t2.timestamp = win_ts(w, b, i);
+        if (cls & C_POSTVOID) t2 = pv_record(t2, d.xr[s.p_tslot[i]], s.amt[i]);
+      }
+      d.xr[slot] = t2;
+      x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
+      uint8_t st = 0;
+      if (t2.flags & TB_TRANSFER_PENDING) {
+        st = wev ? s.bstatus[i] : (uint8_t)TB_PENDING_PENDING;
+        if (t2.timeout > 0) {
+          const uint64_t expires_at = expires_at_of(t2);
+          atomicMin(reinterpret_cast<unsigned long long*>(&d.g->pulse_next), (unsigned long long)expires_at);
+          const bool visible = !(t2.timestamp >> 63) && expires_at <= TB_TIMESTAMP_MAX;
+          if (st == TB_PENDING_PENDING && visible) {
+            const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), 1ull);
+            ExpEntry e;
+            e.expires_at = expires_at;
+            e.slot = (uint32_t)slot;
+            e.pad = 0;
+            d.exp[*d.exp_cur][q] = e;
+          }
+        }
+      }
+      d.xstatus[slot] = st;
+    }
+    for (int k = 0; k < nadd; k++) adds[k].finish();
+  } else {
+    const tb_account_t* ev = reinterpret_cast<const tb_account_t*>(ev_bytes);
+    if (ins) {
+      const uint64_t slot = xbase + rins;
+      tb_account_t a = ev[i];
+      a.timestamp = win_ts(w, b, i);
+      d.acc[slot] = a;
+      d.hot[slot] = 0;
+      acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
+    }
+  }
+  if (i == E - 1) {
+    // the window's last event: totals and window-level state
+    const uint32_t total_bad = rbad + bad, total_ins = rins + (ins ? 1u : 0u);
+    for (int32_t bb = (int32_t)w.nb; bb >= 0 && w.off[bb] == E; bb--) o.batch_base[bb] = total_bad;
+    if (o.out_count) *o.out_count = total_bad;
+    Globals* gw = d.g;
+    gw->result_count = total_bad;
+    if (XFER) {
+      gw->x_count = xbase + total_ins;
+      const u128 sum = gw->ovf_bound + gw->batch_amount_sum;
+      gw->ovf_bound = (gw->batch_huge || sum < gw->ovf_bound) ? MAX128 : sum;
+      gw->batch_amount_sum = 0;
+      gw->batch_huge = 0;
+    } else {
+      gw->acc_count = xbase + total_ins;
     }
   }
 }

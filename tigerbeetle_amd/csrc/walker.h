@@ -6,29 +6,52 @@
 #include "sm_logic.h"
 #include "window.h"
 
-// Batch-local key map helpers (keys are never stored; see BEntry).
-__device__ inline tb_uint128_t bkey(const uint8_t* ev, uint32_t owner) {
-  const uint32_t idx = owner & 0x7FFFFFFFu;
-  return *reinterpret_cast<const tb_uint128_t*>(ev + (size_t)idx * 128 + ((owner >> 31) ? 64 : 0));
+// Window key map (see BEntry). `epoch` is the window number.
+__device__ inline tb_uint128_t bkey(const uint8_t* ev, uint32_t owner, uint32_t is_pid) {
+  return *reinterpret_cast<const tb_uint128_t*>(ev + (size_t)owner * 128 + (is_pid ? 64 : 0));
 }
 
-__device__ inline uint32_t bmap_claim(BEntry* bm, uint32_t mask, const uint8_t* ev, tb_uint128_t key,
-                                      uint32_t owner) {
+// Claims (or finds) the entry of `key` and bumps its id or pending_id count (saturating at 3).
+__device__ inline uint32_t bmap_claim(BEntry* bm, uint32_t mask, const uint8_t* ev, tb_uint128_t key, uint32_t idx,
+                                      uint32_t is_pid, uint32_t epoch) {
+  const unsigned long long inc = is_pid ? (1ull << 23) : (1ull << 21);
   uint32_t h = (uint32_t)hash_id(key.lo, key.hi) & mask;
   for (;;) {
-    const uint32_t old = atomicCAS(&bm[h].owner, NONE32, owner);
-    if (old == NONE32) return h;
-    const tb_uint128_t k = bkey(ev, old);
-    if (k.lo == key.lo && k.hi == key.hi) return h;
+    unsigned long long old = __hip_atomic_load(&bm[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if (bk_epoch(old) != epoch) {
+        const unsigned long long fresh =
+            ((unsigned long long)epoch << 32) | ((unsigned long long)is_pid << 20) | idx | inc;
+        const unsigned long long prev = atomicCAS(&bm[h].key, old, fresh);
+        if (prev == old) return h;
+        old = prev;
+        continue;
+      }
+      const tb_uint128_t k = bkey(ev, bk_owner(old), bk_is_pid(old));
+      if (k.lo != key.lo || k.hi != key.hi) break;  // another key: probe on
+      if ((is_pid ? bk_pidc(old) : bk_idc(old)) == 3) return h;
+      const unsigned long long prev = atomicCAS(&bm[h].key, old, old + inc);
+      if (prev == old) return h;
+      old = prev;
+    }
     h = (h + 1) & mask;
   }
 }
 
-__device__ inline void bmap_reset(BEntry* bm, uint32_t e) {
-  bm[e].owner = NONE32;
-  bm[e].id_count = 0;
-  bm[e].pid_count = 0;
-  bm[e].committed = -1;
+__device__ inline uint32_t bmap_idc(const BEntry* bm, uint32_t e, uint32_t epoch) {
+  const unsigned long long k = bm[e].key;
+  return bk_epoch(k) == epoch ? bk_idc(k) : 0;
+}
+__device__ inline uint32_t bmap_pidc(const BEntry* bm, uint32_t e, uint32_t epoch) {
+  const unsigned long long k = bm[e].key;
+  return bk_epoch(k) == epoch ? bk_pidc(k) : 0;
+}
+__device__ inline int32_t bmap_committed(const BEntry* bm, uint32_t e, uint32_t epoch) {
+  const unsigned long long c = bm[e].commit;
+  return bk_epoch(c) == epoch ? (int32_t)(uint32_t)c : -1;
+}
+__device__ inline void bmap_set_committed(BEntry* bm, uint32_t e, uint32_t epoch, int32_t i) {
+  bm[e].commit = ((unsigned long long)epoch << 32) | (uint32_t)i;
 }
 
 struct Walker {
@@ -36,6 +59,7 @@ struct Walker {
   Scratch s;
   const uint8_t* ev;
   const WinDesc* w;
+  uint32_t epoch;
   uint32_t undo_n;
   bool scope;
 
@@ -71,7 +95,7 @@ struct Walker {
         } break;
         case UNDO_XST: d.xstatus[r.a] = (uint8_t)r.old[0]; break;
         case UNDO_BST: s.bstatus[r.a] = (uint8_t)r.old[0]; break;
-        case UNDO_COMMIT: s.bmap[r.a].committed = (int32_t)(uint32_t)r.old[0]; break;
+        case UNDO_COMMIT: s.bmap[r.a].commit = (unsigned long long)r.old[0]; break;
         case UNDO_INS: s.ins[r.a] = 0; break;
       }
     }
@@ -82,8 +106,8 @@ struct Walker {
     log_small(UNDO_INS, i, 0);
     s.ins[i] = 1;
     const uint32_t e = s.id_ent[i];
-    log_small(UNDO_COMMIT, e, (uint32_t)s.bmap[e].committed);
-    s.bmap[e].committed = (int32_t)i;
+    log_small(UNDO_COMMIT, e, s.bmap[e].commit);
+    bmap_set_committed(s.bmap, e, epoch, (int32_t)i);
   }
 
   // create_transfer (:1462-1585) from the exists check on; validation results come from k_ct_prep.
@@ -93,7 +117,7 @@ struct Walker {
     t.timestamp = win_ts(*w, s.batch[i], i);
     if (cls & C_POSTVOID) return post_or_void(i, t);
     if (s.id_tslot[i] != NONE32) return ct_exists(t, d.xr[s.id_tslot[i]]);
-    const int32_t c = s.bmap[s.id_ent[i]].committed;
+    const int32_t c = bmap_committed(s.bmap, s.id_ent[i], epoch);
     if (c >= 0) return ct_exists(t, s.t2[c]);
     const uint32_t drs = s.dr_slot[i], crs = s.cr_slot[i];
     tb_account_t* dra = &d.acc[drs];
@@ -130,7 +154,7 @@ struct Walker {
       drs = s.dr_slot[i];
       crs = s.cr_slot[i];
     } else {
-      pc = s.bmap[s.pid_ent[i]].committed;
+      pc = bmap_committed(s.bmap, s.pid_ent[i], epoch);
       if (pc < 0) return TB_CT_PENDING_TRANSFER_NOT_FOUND;
       p = s.t2[pc];
       drs = s.dr_slot[pc];
@@ -140,7 +164,7 @@ struct Walker {
     uint32_t r = pv_against(t, p, &amount);
     if (r != CONT) return r;
     if (s.id_tslot[i] != NONE32) return pv_exists(t, d.xr[s.id_tslot[i]], p);
-    const int32_t c = s.bmap[s.id_ent[i]].committed;
+    const int32_t c = bmap_committed(s.bmap, s.id_ent[i], epoch);
     if (c >= 0) return pv_exists(t, s.t2[c], p);
     r = pv_status(pc >= 0 ? s.bstatus[pc] : d.xstatus[pslot]);
     if (r != CONT) return r;
@@ -177,12 +201,12 @@ struct Walker {
     if (s.id_tslot[i] != NONE32) return s.code[i];  // exists before the window: static
     const tb_account_t* evs = reinterpret_cast<const tb_account_t*>(ev);
     const uint32_t e = s.id_ent[i];
-    const int32_t c = s.bmap[e].committed;
+    const int32_t c = bmap_committed(s.bmap, e, epoch);
     if (c >= 0) return ca_exists(evs[i], evs[c]);
     log_small(UNDO_INS, i, 0);
     s.ins[i] = 1;
-    log_small(UNDO_COMMIT, e, (uint32_t)c);
-    s.bmap[e].committed = (int32_t)i;
+    log_small(UNDO_COMMIT, e, s.bmap[e].commit);
+    bmap_set_committed(s.bmap, e, epoch, (int32_t)i);
     return TB_CA_OK;
   }
 

@@ -7,8 +7,7 @@
 #include "dev_common.h"
 
 #define MAXB 64
-#define SEG 1024          // events per segment (scan / count granularity)
-#define SEG_THREADS 256   // threads per segment block (4 consecutive events each)
+#define SEG 1024          // events per segment = threads per segment block (one event each)
 
 struct WinDesc {
   uint32_t nb;             // batches in the window
@@ -118,9 +117,11 @@ __device__ inline uint32_t block_sum(uint32_t v, uint32_t* lds) {
   return tot;
 }
 
-// Sum of per-segment counts cnt[0..seg) (the segment's global exclusive offset).
+// Sum of per-segment counts cnt[0..seg) (the segment's global exclusive offset), for a block of
+// NTHREADS threads.
+template <int NTHREADS>
 __device__ inline uint32_t seg_prefix(const uint32_t* cnt, uint32_t seg, uint32_t* lds) {
   uint32_t v = 0;
-  for (uint32_t j = threadIdx.x; j < seg; j += SEG_THREADS) v += cnt[j];
-  return block_sum<SEG_THREADS / 64>(v, lds);
+  for (uint32_t j = threadIdx.x; j < seg; j += NTHREADS) v += cnt[j];
+  return block_sum<NTHREADS / 64>(v, lds);
 }
