@@ -128,6 +128,22 @@ int tbg_timing_collect(tbg_engine *engine, double *ms, uint64_t *launches, uint3
 /* Introspection of the last create_* batch: per-event class bits and final codes (debugging). */
 int tbg_debug_last_batch(tbg_engine *engine, uint32_t *cls, uint32_t *code, uint32_t n);
 
+/* cfg3: accounts with debits_must_not_exceed_credits on rank < limited_top and on ~half the rest
+ * (ranks >= n_accounts are unlimited treasury accounts); funding transfers credit account k from
+ * treasury account k % treasury; Zipf-distributed transfers over a u64 CDF table in HBM
+ * (tigerbeetle_amd.workload.zipf_cdf). */
+int tbg_gen_accounts_cfg3(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
+                          uint64_t limited_top, void *stream);
+int tbg_gen_funding_cfg3(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
+                         uint64_t treasury, uint64_t amount, uint64_t id_offset, void *stream);
+int tbg_gen_transfers_zipf(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
+                           const void *d_cdf, uint64_t id_offset, void *stream);
+/* cfg4: two-phase (30 % pending with 1-60 s timeouts, ~20 % post / ~10 % void of earlier pending
+ * transfers) with ~10 % of events in linked chains of 2-8, a quarter of them with an injected
+ * failure. */
+int tbg_gen_transfers_cfg4(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
+                           uint64_t batch, uint64_t id_offset, void *stream);
+
 /* Library build identification ("gfx950 ..."). */
 const char *tbg_version(void);
 

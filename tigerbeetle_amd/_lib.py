@@ -14,7 +14,8 @@ EXPORTS = [
     "tbg_commit_device", "tbg_commit_window", "tbg_sync", "tbg_stream", "tbg_setup_balances", "tbg_get_stats",
     "tbg_dump_accounts", "tbg_dump_transfers", "tbg_dump_transfer_status", "tbg_device_stores",
     "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_version", "tbg_debug_last_batch",
-    "tbg_timing_enable", "tbg_timing_collect",
+    "tbg_timing_enable", "tbg_timing_collect", "tbg_gen_accounts_cfg3", "tbg_gen_funding_cfg3",
+    "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4",
 ]
 
 
@@ -80,6 +81,10 @@ def lib():
         "tbg_debug_last_batch": ([vp, vp, vp, u32], i32),
         "tbg_timing_enable": ([vp, ctypes.c_int], i32),
         "tbg_timing_collect": ([vp, vp, vp, u32], i32),
+        "tbg_gen_accounts_cfg3": ([vp, u64, u64, u64, u64, u64, vp], i32),
+        "tbg_gen_funding_cfg3": ([vp, u64, u64, u64, u64, u64, u64, u64, vp], i32),
+        "tbg_gen_transfers_zipf": ([vp, u64, u64, u64, u64, vp, u64, vp], i32),
+        "tbg_gen_transfers_cfg4": ([vp, u64, u64, u64, u64, u64, u64, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

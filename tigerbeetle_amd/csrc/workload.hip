@@ -102,3 +102,233 @@ extern "C" int tbg_gen_transfers_uniform(void* d_out, uint64_t first, uint64_t c
       (tb_transfer_t*)d_out, first, count, seed, n_accounts, id_offset);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+// ------------------------------------------------------------------------------------------------
+// cfg3: Zipf(s) hot accounts with debits_must_not_exceed_credits limits.
+//   accounts: rank r (id r+1) is limited iff r < limited_top or bit 0 of rnd(seed, r, 7) is set;
+//             treasury accounts (ids n_accounts+1 .. n_accounts+treasury) are unlimited.
+//   funding:  transfer k (k < n_accounts) credits account k from treasury account k % treasury.
+//   stream:   debit and credit ranks drawn from the Zipf table (u64 CDF thresholds, shared by the
+//             device and numpy generators); an equal credit is redrawn once, then bumped by one.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline bool cfg3_limited(uint64_t seed, uint64_t r, uint64_t limited_top) {
+  return r < limited_top || (wl_rnd(seed, r, 7) & 1);
+}
+
+__device__ inline uint64_t zipf_draw(const uint64_t* cdf, uint64_t n, uint64_t u) {
+  // first k with cdf[k] > u
+  uint64_t lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (cdf[mid] > u)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  return lo;
+}
+
+__global__ void k_gen_accounts_cfg3(tb_account_t* out, uint64_t first, uint64_t count, uint64_t seed,
+                                    uint64_t n_accounts, uint64_t limited_top) {
+  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const uint64_t idx = first + k;
+  tb_account_t a;
+  a.id.lo = idx + 1;
+  a.id.hi = 0;
+  a.debits_pending = {0, 0};
+  a.debits_posted = {0, 0};
+  a.credits_pending = {0, 0};
+  a.credits_posted = {0, 0};
+  a.user_data_128.lo = wl_rnd(seed, idx, 0);
+  a.user_data_128.hi = wl_rnd(seed, idx, 1);
+  a.user_data_64 = wl_rnd(seed, idx, 2);
+  a.user_data_32 = (uint32_t)wl_rnd(seed, idx, 3);
+  a.reserved = 0;
+  a.ledger = 2;
+  a.code = 1;
+  a.flags = (idx < n_accounts && cfg3_limited(seed, idx, limited_top)) ? TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS : 0;
+  a.timestamp = 0;
+  out[k] = a;
+}
+
+__device__ inline void wl_fill_common(tb_transfer_t& t, uint64_t seed, uint64_t idx) {
+  t.pending_id = {0, 0};
+  t.user_data_128.lo = wl_rnd(seed, idx, 14);
+  t.user_data_128.hi = wl_rnd(seed, idx, 15);
+  t.user_data_64 = wl_rnd(seed, idx, 16);
+  t.user_data_32 = (uint32_t)wl_rnd(seed, idx, 17);
+  t.timeout = 0;
+  t.ledger = 2;
+  const uint32_t c = (uint32_t)(wl_rnd(seed, idx, 18) & 0xFFFF) + 1;
+  t.code = (uint16_t)(c > 0xFFFF ? 0xFFFF : c);
+  t.flags = 0;
+  t.timestamp = 0;
+}
+
+__global__ void k_gen_funding_cfg3(tb_transfer_t* out, uint64_t first, uint64_t count, uint64_t seed,
+                                   uint64_t n_accounts, uint64_t treasury, uint64_t amount, uint64_t id_offset) {
+  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const uint64_t idx = first + k;
+  tb_transfer_t t;
+  t.id.lo = id_offset + idx + 1;
+  t.id.hi = 0;
+  t.debit_account_id.lo = n_accounts + (idx % treasury) + 1;
+  t.debit_account_id.hi = 0;
+  t.credit_account_id.lo = idx + 1;
+  t.credit_account_id.hi = 0;
+  t.amount.lo = amount;
+  t.amount.hi = 0;
+  wl_fill_common(t, seed, idx);
+  out[k] = t;
+}
+
+__global__ void k_gen_transfers_zipf(tb_transfer_t* out, uint64_t first, uint64_t count, uint64_t seed,
+                                     uint64_t n_accounts, const uint64_t* cdf, uint64_t id_offset) {
+  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const uint64_t idx = first + k;
+  const uint64_t dr = zipf_draw(cdf, n_accounts, wl_rnd(seed, idx, 20));
+  uint64_t cr = zipf_draw(cdf, n_accounts, wl_rnd(seed, idx, 21));
+  if (cr == dr) cr = zipf_draw(cdf, n_accounts, wl_rnd(seed, idx, 22));
+  if (cr == dr) cr = (cr + 1) % n_accounts;
+  tb_transfer_t t;
+  t.id.lo = id_offset + idx + 1;
+  t.id.hi = 0;
+  t.debit_account_id.lo = dr + 1;
+  t.debit_account_id.hi = 0;
+  t.credit_account_id.lo = cr + 1;
+  t.credit_account_id.hi = 0;
+  t.amount.lo = wl_amount(wl_rnd(seed, idx, 12), wl_rnd(seed, idx, 13));
+  t.amount.hi = 0;
+  wl_fill_common(t, seed, idx);
+  out[k] = t;
+}
+
+// ------------------------------------------------------------------------------------------------
+// cfg4: two-phase + linked chains.
+//   kind(k) by rnd(k, 30) % 100: < 30 pending (timeout 1..60 s), < 50 post, < 60 void, else posted.
+//   post/void target: walk back from k - (1 + rnd(k, 31) % (4 * batch)) to the nearest pending-kind
+//     event (at most 64 steps; none found -> plain transfer). post amount U[0, p.amount] (0 = full),
+//     void amount 0 or p.amount.
+//   chains: slot s = k / 8 hosts a chain when rnd(s, 40) % 100 < 16, of length L = 2 + rnd(s, 41) % 7,
+//     linked on its first L-1 events; a quarter of the chains get one injected failure (member
+//     rnd(s, 43) % L: debit == credit for creates, pending_id = u128 max for post/void).
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline uint32_t cfg4_kind(uint64_t seed, uint64_t k) {
+  const uint32_t r = (uint32_t)(wl_rnd(seed, k, 30) % 100);
+  return r < 30 ? 1u : r < 50 ? 2u : r < 60 ? 3u : 0u;  // 1 pending, 2 post, 3 void, 0 posted
+}
+
+__host__ __device__ inline uint64_t cfg4_amount(uint64_t seed, uint64_t k) {
+  return wl_amount(wl_rnd(seed, k, 12), wl_rnd(seed, k, 13));
+}
+
+__global__ void k_gen_transfers_cfg4(tb_transfer_t* out, uint64_t first, uint64_t count, uint64_t seed,
+                                     uint64_t n_accounts, uint64_t batch, uint64_t id_offset) {
+  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const uint64_t idx = first + k;
+  tb_transfer_t t;
+  t.id.lo = id_offset + idx + 1;
+  t.id.hi = 0;
+  wl_fill_common(t, seed, idx);
+  uint32_t kind = cfg4_kind(seed, idx);
+  int64_t target = -1;
+  if (kind == 2 || kind == 3) {
+    const uint64_t back = 1 + wl_rnd(seed, idx, 31) % (4 * batch);
+    if (back <= idx) {
+      int64_t j = (int64_t)(idx - back);
+      for (int step = 0; step < 64 && j >= 0; step++, j--) {
+        if (cfg4_kind(seed, (uint64_t)j) == 1) {
+          target = j;
+          break;
+        }
+      }
+    }
+    if (target < 0) kind = 0;
+  }
+  const uint64_t dr = wl_rnd(seed, idx, 10) % n_accounts;
+  uint64_t cr = wl_rnd(seed, idx, 11) % n_accounts;
+  if (cr == dr) cr = (cr + 1) % n_accounts;
+  if (kind == 2 || kind == 3) {
+    const uint64_t pa = cfg4_amount(seed, (uint64_t)target);
+    t.debit_account_id = {0, 0};
+    t.credit_account_id = {0, 0};
+    t.pending_id.lo = id_offset + (uint64_t)target + 1;
+    t.pending_id.hi = 0;
+    t.ledger = 0;
+    t.code = 0;
+    if (kind == 2) {
+      t.flags = TB_TRANSFER_POST_PENDING;
+      t.amount.lo = wl_rnd(seed, idx, 32) % (pa + 1);
+    } else {
+      t.flags = TB_TRANSFER_VOID_PENDING;
+      t.amount.lo = (wl_rnd(seed, idx, 32) & 1) ? pa : 0;
+    }
+    t.amount.hi = 0;
+  } else {
+    t.debit_account_id.lo = dr + 1;
+    t.debit_account_id.hi = 0;
+    t.credit_account_id.lo = cr + 1;
+    t.credit_account_id.hi = 0;
+    t.amount.lo = cfg4_amount(seed, idx);
+    t.amount.hi = 0;
+    if (kind == 1) {
+      t.flags = TB_TRANSFER_PENDING;
+      t.timeout = 1 + (uint32_t)(wl_rnd(seed, idx, 33) % 60);
+    }
+  }
+  // chains
+  const uint64_t slot = idx / 8, pos = idx % 8;
+  if (wl_rnd(seed, slot, 40) % 100 < 16) {
+    const uint64_t L = 2 + wl_rnd(seed, slot, 41) % 7;
+    if (pos < L) {
+      if (pos + 1 < L) t.flags |= TB_TRANSFER_LINKED;
+      if (wl_rnd(seed, slot, 42) % 4 == 0 && pos == wl_rnd(seed, slot, 43) % L) {
+        if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
+          t.pending_id.lo = ~0ull;
+          t.pending_id.hi = ~0ull;
+        } else {
+          t.credit_account_id = t.debit_account_id;
+        }
+      }
+    }
+  }
+  out[k] = t;
+}
+
+#define WL_GRID(count) (unsigned)(((count) + 255) / 256), 256
+
+extern "C" int tbg_gen_accounts_cfg3(void* d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
+                                     uint64_t limited_top, void* stream) {
+  if (!count) return 0;
+  k_gen_accounts_cfg3<<<WL_GRID(count), 0, (hipStream_t)stream>>>((tb_account_t*)d_out, first, count, seed,
+                                                                  n_accounts, limited_top);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int tbg_gen_funding_cfg3(void* d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
+                                    uint64_t treasury, uint64_t amount, uint64_t id_offset, void* stream) {
+  if (!count) return 0;
+  k_gen_funding_cfg3<<<WL_GRID(count), 0, (hipStream_t)stream>>>((tb_transfer_t*)d_out, first, count, seed,
+                                                                 n_accounts, treasury, amount, id_offset);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int tbg_gen_transfers_zipf(void* d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
+                                      const void* d_cdf, uint64_t id_offset, void* stream) {
+  if (!count) return 0;
+  k_gen_transfers_zipf<<<WL_GRID(count), 0, (hipStream_t)stream>>>((tb_transfer_t*)d_out, first, count, seed,
+                                                                   n_accounts, (const uint64_t*)d_cdf, id_offset);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int tbg_gen_transfers_cfg4(void* d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
+                                      uint64_t batch, uint64_t id_offset, void* stream) {
+  if (!count) return 0;
+  k_gen_transfers_cfg4<<<WL_GRID(count), 0, (hipStream_t)stream>>>((tb_transfer_t*)d_out, first, count, seed,
+                                                                   n_accounts, batch, id_offset);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

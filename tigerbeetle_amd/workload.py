@@ -66,3 +66,135 @@ def transfers_uniform(first, count, seed, n_accounts, id_offset=0):
     c = (rnd(seed, idx, 18) & np.uint64(0xFFFF)) + np.uint64(1)
     t["code"] = np.minimum(c, np.uint64(0xFFFF)).astype(np.uint16)
     return t
+
+
+# ------------------------------------------------------------------------------------------------
+# cfg3: Zipf hot accounts with debits_must_not_exceed_credits limits (see csrc/workload.hip).
+# ------------------------------------------------------------------------------------------------
+def zipf_cdf(n, s=1.2):
+    """u64 thresholds: draw k = first index with cdf[k] > u for a uniform u64 u."""
+    w = np.arange(1, n + 1, dtype=np.float64) ** (-s)
+    c = np.cumsum(w)
+    c /= c[-1]
+    thr = (c * 2.0 ** 63).astype(np.uint64) << np.uint64(1)
+    thr[-1] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    return thr
+
+
+def zipf_draw(cdf, u):
+    k = np.searchsorted(cdf, u, side="right")
+    return np.minimum(k, len(cdf) - 1).astype(np.uint64)
+
+
+def cfg3_limited(seed, r, limited_top):
+    r = np.asarray(r, np.uint64)
+    return (r < np.uint64(limited_top)) | ((rnd(seed, r, 7) & np.uint64(1)) == 1)
+
+
+def accounts_cfg3(first, count, seed, n_accounts, limited_top):
+    a = accounts(first, count, seed, ledger=2, code=1, flags=0)
+    idx = np.arange(first, first + count, dtype=np.uint64)
+    lim = cfg3_limited(seed, idx, limited_top) & (idx < np.uint64(n_accounts))
+    a["flags"] = np.where(lim, 2, 0).astype(np.uint16)
+    return a
+
+
+def _common(t, seed, idx):
+    t["user_data_128_lo"] = rnd(seed, idx, 14)
+    t["user_data_128_hi"] = rnd(seed, idx, 15)
+    t["user_data_64"] = rnd(seed, idx, 16)
+    t["user_data_32"] = (rnd(seed, idx, 17) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    t["ledger"] = 2
+    c = (rnd(seed, idx, 18) & np.uint64(0xFFFF)) + np.uint64(1)
+    t["code"] = np.minimum(c, np.uint64(0xFFFF)).astype(np.uint16)
+
+
+def funding_cfg3(first, count, seed, n_accounts, treasury, amount, id_offset):
+    idx = np.arange(first, first + count, dtype=np.uint64)
+    t = np.zeros(count, TRANSFER_DTYPE)
+    t["id_lo"] = np.uint64(id_offset) + idx + np.uint64(1)
+    t["debit_account_id_lo"] = np.uint64(n_accounts) + idx % np.uint64(treasury) + np.uint64(1)
+    t["credit_account_id_lo"] = idx + np.uint64(1)
+    t["amount_lo"] = np.uint64(amount)
+    _common(t, seed, idx)
+    return t
+
+
+def transfers_zipf(first, count, seed, n_accounts, cdf, id_offset=0):
+    idx = np.arange(first, first + count, dtype=np.uint64)
+    n = np.uint64(n_accounts)
+    dr = zipf_draw(cdf, rnd(seed, idx, 20))
+    cr = zipf_draw(cdf, rnd(seed, idx, 21))
+    cr = np.where(cr == dr, zipf_draw(cdf, rnd(seed, idx, 22)), cr)
+    cr = np.where(cr == dr, (cr + np.uint64(1)) % n, cr)
+    t = np.zeros(count, TRANSFER_DTYPE)
+    t["id_lo"] = np.uint64(id_offset) + idx + np.uint64(1)
+    t["debit_account_id_lo"] = dr + np.uint64(1)
+    t["credit_account_id_lo"] = cr + np.uint64(1)
+    t["amount_lo"] = amount(rnd(seed, idx, 12), rnd(seed, idx, 13))
+    _common(t, seed, idx)
+    return t
+
+
+# ------------------------------------------------------------------------------------------------
+# cfg4: two-phase + linked chains (see csrc/workload.hip).
+# ------------------------------------------------------------------------------------------------
+def cfg4_kind(seed, k):
+    r = rnd(seed, k, 30) % np.uint64(100)
+    return np.where(r < 30, 1, np.where(r < 50, 2, np.where(r < 60, 3, 0))).astype(np.int64)
+
+
+def transfers_cfg4(first, count, seed, n_accounts, batch, id_offset=0):
+    idx = np.arange(first, first + count, dtype=np.uint64)
+    n = np.uint64(n_accounts)
+    t = np.zeros(count, TRANSFER_DTYPE)
+    t["id_lo"] = np.uint64(id_offset) + idx + np.uint64(1)
+    _common(t, seed, idx)
+    kind = cfg4_kind(seed, idx)
+    back = np.uint64(1) + rnd(seed, idx, 31) % np.uint64(4 * batch)
+    pv = (kind == 2) | (kind == 3)
+    ok = pv & (back <= idx)
+    j = np.where(ok, idx.astype(np.int64) - back.astype(np.int64), -1)
+    target = np.full(count, -1, np.int64)
+    for _ in range(64):
+        live = ok & (target < 0) & (j >= 0)
+        if not live.any():
+            break
+        kj = cfg4_kind(seed, np.maximum(j, 0).astype(np.uint64))
+        hit = live & (kj == 1)
+        target = np.where(hit, j, target)
+        j = np.where(live & ~hit, j - 1, j)
+    kind = np.where(pv & (target < 0), 0, kind)
+    pv = (kind == 2) | (kind == 3)
+    dr = rnd(seed, idx, 10) % n
+    cr = rnd(seed, idx, 11) % n
+    cr = np.where(cr == dr, (cr + np.uint64(1)) % n, cr)
+    tgt = np.maximum(target, 0).astype(np.uint64)
+    pa = amount(rnd(seed, tgt, 12), rnd(seed, tgt, 13))
+    own = amount(rnd(seed, idx, 12), rnd(seed, idx, 13))
+    r32 = rnd(seed, idx, 32)
+    post_amt = r32 % (pa + np.uint64(1))
+    void_amt = np.where((r32 & np.uint64(1)) == 1, pa, np.uint64(0))
+    t["debit_account_id_lo"] = np.where(pv, 0, dr + np.uint64(1))
+    t["credit_account_id_lo"] = np.where(pv, 0, cr + np.uint64(1))
+    t["pending_id_lo"] = np.where(pv, np.uint64(id_offset) + tgt + np.uint64(1), 0)
+    t["ledger"] = np.where(pv, 0, 2)
+    t["code"] = np.where(pv, 0, t["code"])
+    t["amount_lo"] = np.where(kind == 2, post_amt, np.where(kind == 3, void_amt, own))
+    flags = np.where(kind == 1, 2, np.where(kind == 2, 4, np.where(kind == 3, 8, 0))).astype(np.uint16)
+    t["timeout"] = np.where(kind == 1, (np.uint64(1) + rnd(seed, idx, 33) % np.uint64(60)), 0).astype(np.uint32)
+    # chains
+    slot = idx // np.uint64(8)
+    pos = idx % np.uint64(8)
+    chain = (rnd(seed, slot, 40) % np.uint64(100)) < np.uint64(16)
+    L = np.uint64(2) + rnd(seed, slot, 41) % np.uint64(7)
+    member = chain & (pos < L)
+    flags = np.where(member & (pos + np.uint64(1) < L), flags | 1, flags).astype(np.uint16)
+    inject = member & ((rnd(seed, slot, 42) % np.uint64(4)) == 0) & (pos == rnd(seed, slot, 43) % L)
+    inj_pv = inject & pv
+    inj_cr = inject & ~pv
+    t["pending_id_lo"] = np.where(inj_pv, np.uint64(0xFFFFFFFFFFFFFFFF), t["pending_id_lo"])
+    t["pending_id_hi"] = np.where(inj_pv, np.uint64(0xFFFFFFFFFFFFFFFF), 0)
+    t["credit_account_id_lo"] = np.where(inj_cr, t["debit_account_id_lo"], t["credit_account_id_lo"])
+    t["flags"] = flags
+    return t
