@@ -36,7 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BATCH = 8190
-PHASES = ["prep", "link", "classify", "wcount", "wlist", "walk", "final", "pulse"]
+PHASES = ["prep", "resolve", "classify", "wcount", "wlist", "walk", "final", "pulse"]
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
 NS_PER_S = 1_000_000_000
 

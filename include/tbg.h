@@ -31,8 +31,11 @@ typedef struct tbg_config {
     uint64_t accounts_max;   /* capacity of the account store */
     uint64_t transfers_max;  /* capacity of the transfer store */
     uint32_t window_events_max; /* events per commit window (tbg_commit_window); 0 = batch_max */
-    uint32_t reserved;
+    uint32_t flags;          /* TBG_FLAG_* */
 } tbg_config;
+
+/* Decide balance-limit windows on the sequential walker only (no account-parallel resolver). */
+#define TBG_FLAG_NO_RESOLVER 1u
 
 #define TBG_OK 0
 #define TBG_E_INVALID (-1)   /* input_valid() would reject the request */
@@ -100,6 +103,7 @@ typedef struct tbg_stats {
     uint64_t pulse_next_timestamp;
     uint64_t events_total;    /* create_* events committed through the engine */
     uint64_t walker_events;   /* of which ran on the sequential walker */
+    uint64_t resolver_events; /* of which the account-parallel resolver decided */
 } tbg_stats;
 int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
 

@@ -30,13 +30,17 @@ def u128(v):
 class Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("batch_max", ctypes.c_uint32),
                 ("accounts_max", ctypes.c_uint64), ("transfers_max", ctypes.c_uint64),
-                ("window_events_max", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("window_events_max", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+FLAG_NO_RESOLVER = 1
 
 
 class Stats(ctypes.Structure):
     _fields_ = [("accounts", ctypes.c_uint64), ("transfers", ctypes.c_uint64),
                 ("expiry_entries", ctypes.c_uint64), ("pulse_next_timestamp", ctypes.c_uint64),
-                ("events_total", ctypes.c_uint64), ("walker_events", ctypes.c_uint64)]
+                ("events_total", ctypes.c_uint64), ("walker_events", ctypes.c_uint64),
+                ("resolver_events", ctypes.c_uint64)]
 
 
 _lib = None

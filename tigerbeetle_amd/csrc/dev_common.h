@@ -92,6 +92,15 @@ struct __attribute__((aligned(64))) Globals {
   // walker statistics (cumulative)
   uint64_t w_events_total;
   uint64_t events_total;
+  // account-parallel resolver (resolver.h), per window; reset by k_final's last event
+  uint32_t hot_count;   // hot accounts this window (dense ranks 0..hot_count-1)
+  uint32_t res_inelig;  // some W event is outside the resolver's class
+  uint32_t res_error;   // a resolver wave gave up (bounded spin): the sequential walker runs instead
+  uint32_t res_done;    // the resolver decided every W event
+  uint32_t heavy_count; // hot ranks walked by a whole wave (long entry lists)
+  uint32_t light_count; // hot ranks walked by one lane
+  uint64_t res_events_total;  // cumulative W events decided by the resolver
+  uint64_t limited_accounts;  // accounts created with a balance-limit flag (cumulative)
 };
 
 // Per-event class bits (scratch `cls`).
@@ -111,6 +120,9 @@ enum : uint32_t {
   C_PV_PREBATCH = 1u << 12,// post/void whose pending transfer was found in the pre-batch table
   C_COMMIT = 1u << 13,     // final: effects persist (set by the scan kernel)
   C_INSERTED = 1u << 14,   // final: record inserted (ok, or the expired-post quirk)
+  C_BAL = 1u << 15,        // balancing_debit or balancing_credit
+  C_RES_DR = 1u << 16,     // final: the resolver applied this event's debit-account effects
+  C_RES_CR = 1u << 17,     // final: the resolver applied this event's credit-account effects
 };
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

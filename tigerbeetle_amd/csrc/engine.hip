@@ -31,10 +31,13 @@
 #include <new>
 #include <vector>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "../../include/tbg.h"
 #include "dev_common.h"
 #include "sm_logic.h"
 #include "walker.h"
+#include "resolver.h"
 #include "window.h"
 
 // Probe continuation after a first entry was already loaded (lets the first probes of several
@@ -68,6 +71,23 @@ __device__ inline void check_window(const WinDesc& w, Globals* g) {
   const uint64_t last = w.T[w.nb - 1];
   const uint64_t first_ts = win_ts(w, 0, w.off[0]);
   if (last >= g->pulse_next || last >= first_ts + TB_NS_PER_S) g->window_error = 1;
+}
+
+// A balance-reading decision makes the read account hot for this window: every event touching it
+// is then decided in order (resolver.h or the walker). The first marker assigns the account its
+// dense rank (one counter atomic per wave).
+__device__ inline void mark_hot(Dev d, uint32_t slot, uint32_t epoch) {
+  // a plain read first: a hot account is marked by many events (a stale read only costs the atomic)
+  bool first = false;
+  if (d.hot[slot] != epoch) first = atomicExch(&d.hot[slot], epoch) != epoch;
+  const unsigned long long m = __ballot(first);
+  if (!first) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(&d.g->hot_count, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  d.hot_rank[slot] = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -172,14 +192,11 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
               if (f & TB_TRANSFER_PENDING) cls |= C_PENDING;
               // A balance-reading decision makes the read account hot for this window (every event
               // touching it then runs on the walker, in order).
-              if ((de.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) || (f & TB_TRANSFER_BALANCING_DEBIT)) {
+              if ((de.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) || (f & TB_TRANSFER_BALANCING_DEBIT))
                 cls |= C_READS_DR;
-                d.hot[dr_slot] = epoch;
-              }
-              if ((ce.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) || (f & TB_TRANSFER_BALANCING_CREDIT)) {
+              if ((ce.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) || (f & TB_TRANSFER_BALANCING_CREDIT))
                 cls |= C_READS_CR;
-                d.hot[cr_slot] = epoch;
-              }
+              if (f & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT)) cls |= C_BAL;
               amt = U(t.amount);
               // Overflow checks cannot fail in an overflow-free window (checked in k_classify).
               if (ovf64(t.timestamp, (uint64_t)t.timeout * TB_NS_PER_S)) {
@@ -194,6 +211,9 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
       }
     }
     if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&huge_any, 1u);
+    // Hot marks: the first marker of an account this window gives it the next dense rank.
+    if (cls & C_READS_DR) mark_hot(d, dr_slot, epoch);
+    if (cls & C_READS_CR) mark_hot(d, cr_slot, epoch);
     s.code[i] = code;
     s.cls[i] = cls;
     s.batch[i] = (uint16_t)b;
@@ -303,25 +323,31 @@ __device__ inline bool is_w(const Dev& d, const Scratch& s, uint32_t j, uint32_t
   return (dr != NONE32 && d.hot[dr] == epoch) || (cr != NONE32 && d.hot[cr] == epoch);
 }
 
+// A W event outside the resolver's class (resolver.h) sends the whole window to the walker.
+__device__ inline bool res_bad(const Scratch& s, uint32_t j, uint32_t cls, uint32_t epoch) {
+  if (cls & (C_LINKED | C_POSTVOID | C_BAL)) return true;
+  if (!(cls & C_REACH)) return false;
+  const uint32_t e = s.id_ent[j];
+  return bmap_idc(s.bmap, e, epoch) > 1 || bmap_pidc(s.bmap, e, epoch) > 0;
+}
+
 template <bool XFER>
-__global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, uint32_t epoch) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= w.E) return;
-  const bool ovf_mode = XFER && window_ovf_mode(d.g);
+__device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinDesc& w, uint32_t i, uint32_t epoch,
+                                      bool ovf_mode) {
   const uint32_t b = s.batch[i];
   const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
   uint32_t cls = s.cls[i];
   const bool linked = cls & C_LINKED;
-  if (i != first && (s.cls[i - 1] & C_LINKED)) return;  // chain member: its head decides
+  if (i != first && (s.cls[i - 1] & C_LINKED)) return false;  // chain member: its head decides
   if (!linked) {
     // singleton (:1255-1259, :1289-1290)
     if (is_w<XFER>(d, s, i, &cls, epoch, ovf_mode)) {
       s.cls[i] = cls | C_W;
-    } else {
-      const uint32_t code = s.code[i];
-      s.cls[i] = cls | (code == TB_CT_OK ? C_COMMIT : 0) | ((cls & C_INSERT) ? C_INSERTED : 0);
+      return res_bad(s, i, cls, epoch);
     }
-    return;
+    const uint32_t code = s.code[i];
+    s.cls[i] = cls | (code == TB_CT_OK ? C_COMMIT : 0) | ((cls & C_INSERT) ? C_INSERTED : 0);
+    return false;
   }
   // chain head: members i..end, end = first unlinked event or the batch's last event (:1240-1300)
   uint32_t end = i;
@@ -351,6 +377,21 @@ __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, u
     s.code[j] = code;
     s.cls[j] = cj | (commit ? C_COMMIT : 0) | ((commit && (cj & C_INSERT)) ? C_INSERTED : 0);
   }
+  return any_w;  // a chain in W: walker
+}
+
+template <bool XFER>
+__global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, uint32_t epoch) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ovf_mode = XFER && window_ovf_mode(d.g);
+  bool bad = false;
+  if (i < w.E) bad = classify_event<XFER>(d, s, w, i, epoch, ovf_mode);
+  if (XFER && i == 0) {
+    // the resolver's 128-bit signed arithmetic needs every balance sum below 2^126
+    const u128 sum = d.g->ovf_bound + d.g->batch_amount_sum;
+    if (ovf_mode || (sum >> 126) != 0) bad = true;
+  }
+  if (XFER && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(&d.g->res_inelig, 1u);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -409,7 +450,12 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
     if (threadIdx.x == 0) d.g->events_total += w.E;
     return;
   }
-  if (threadIdx.x == 0) {
+  const bool resolved = XFER && d.g->res_done;  // resolver.h decided every W event
+  if (threadIdx.x == 0 && resolved) {
+    d.g->res_events_total += w_count;
+    d.g->events_total += w.E;
+  }
+  if (threadIdx.x == 0 && !resolved) {
     Walker wk;
     wk.d = d;
     wk.s = s;
@@ -508,7 +554,13 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
       tb_account_t* dra = &d.acc[s.dr_slot[i]];
       tb_account_t* cra = &d.acc[s.cr_slot[i]];
       const u128 a = s.amt[i];
-      if (cls & C_POSTVOID) {
+      if (cls & (C_RES_DR | C_RES_CR)) {
+        // decided by the resolver, which applied the hot side(s); only a plain single-phase or
+        // pending create reaches here
+        const bool pend = cls & C_PENDING;
+        if (!(cls & C_RES_DR)) adds[nadd++].issue(pend ? &dra->debits_pending : &dra->debits_posted, a);
+        if (!(cls & C_RES_CR)) adds[nadd++].issue(pend ? &cra->credits_pending : &cra->credits_posted, a);
+      } else if (cls & C_POSTVOID) {
         const u128 pa = s.pamt[i];
         adds[nadd++].issue(&dra->debits_pending, (u128)0 - pa);
         adds[nadd++].issue(&cra->credits_pending, (u128)0 - pa);
@@ -566,6 +618,8 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
       d.acc[slot] = a;
       d.hot[slot] = 0;
       acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
+      if (a.flags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS | TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS))
+        atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->limited_accounts), 1ull);
     }
   }
   if (i == E - 1) {
@@ -584,6 +638,12 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     } else {
       gw->acc_count = xbase + total_ins;
     }
+    gw->hot_count = 0;
+    gw->res_inelig = 0;
+    gw->res_error = 0;
+    gw->res_done = 0;
+    gw->heavy_count = 0;
+    gw->light_count = 0;
   }
 }
 

@@ -44,6 +44,7 @@ struct Dev {
   uint64_t acc_mask;
   tb_account_t* acc;
   uint32_t* hot;  // per account slot: epoch of the last window that marked it hot
+  uint32_t* hot_rank;  // per account slot: its dense rank among this window's hot accounts
   XEntry* x_tab;
   uint64_t x_mask;
   tb_transfer_t* xr;
@@ -64,6 +65,15 @@ struct Scratch {
   UndoRec* undo;
   uint32_t *cnt_w, *cnt_bad, *cnt_ins;  // per segment
   ExpEntry* cand;
+  // account-parallel resolver (resolver.h)
+  uint32_t *rkey_in, *rval_in, *rkey, *rval;  // (hot rank, 2*event+side) pairs, then sorted by rank
+  uint32_t* rmeta;                            // sorted entries: event | side | check | wait
+  u128* ramt;                                 // sorted entries: amount
+  struct RState* rstate;                      // per hot rank: segment, cursor, available balance
+  uint32_t* st;                               // per event: published limit-check outcomes
+  uint32_t *heavy, *light;                    // hot ranks by walker kind
+  void* sort_tmp;
+  size_t sort_tmp_bytes;
 };
 
 // ------------------------------------------------------------------------------------------------

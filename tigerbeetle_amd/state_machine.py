@@ -17,9 +17,10 @@ MESSAGE_BODY_SIZE_MAX = 1048576 - 256
 
 class StateMachine:
     def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20,
-                 window_events_max=0):
+                 window_events_max=0, resolver=True):
         L = _lib.lib()
-        cfg = _lib.Config(device, batch_max, accounts_max, transfers_max, window_events_max, 0)
+        flags = 0 if resolver else _lib.FLAG_NO_RESOLVER
+        cfg = _lib.Config(device, batch_max, accounts_max, transfers_max, window_events_max, flags)
         h = ctypes.c_void_p()
         _lib.check(L.tbg_create(ctypes.byref(cfg), ctypes.byref(h)), "tbg_create")
         self.h = h
