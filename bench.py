@@ -308,6 +308,10 @@ def main():
         all_events, all_fails = float(timed_events), float(timed_fails)
 
     stats = sm.stats()
+    dbg = (ctypes.c_uint64 * 8)()
+    L.tbg_debug_counters(sm.h, dbg, 8)
+    if os.environ.get("TBG_DEBUG"):
+        print("resolver counters", list(dbg), file=sys.stderr)
     if args.verify:
         assert acc_fail == 0 and setup_fail == 0, (acc_fail, setup_fail)
         if cfg in ("cfg1", "cfg2"):

@@ -36,6 +36,8 @@ typedef struct tbg_config {
 
 /* Decide balance-limit windows on the sequential walker only (no account-parallel resolver). */
 #define TBG_FLAG_NO_RESOLVER 1u
+/* Walk W events on the single sequential walker only (no component-parallel walkers). */
+#define TBG_FLAG_NO_COMPONENTS 2u
 
 #define TBG_OK 0
 #define TBG_E_INVALID (-1)   /* input_valid() would reject the request */
@@ -104,8 +106,12 @@ typedef struct tbg_stats {
     uint64_t events_total;    /* create_* events committed through the engine */
     uint64_t walker_events;   /* of which ran on the sequential walker */
     uint64_t resolver_events; /* of which the account-parallel resolver decided */
+    uint64_t component_events; /* of which component-parallel walkers decided */
 } tbg_stats;
 int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
+
+/* Debug: cumulative resolver counters (see host.inc); up to 8 values. */
+int tbg_debug_counters(tbg_engine *engine, uint64_t *out, uint32_t n);
 
 /* Whole-state dumps in creation (= timestamp) order, for parity checks. */
 int tbg_dump_accounts(tbg_engine *engine, tb_account_t *out, uint64_t cap, uint64_t *count);

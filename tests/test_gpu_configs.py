@@ -105,6 +105,8 @@ def test_cfg4_two_phase_chains_parity():
         # rollbacks, expiry and two-phase outcomes all occur
         assert {1, 12, 15, 35}.issubset(codes), codes
         _compare_final(gpu, ref)
+        st = gpu.stats()
+        assert st["component_events"] > 0 and st["walker_events"] == 0, st
     finally:
         gpu.close()
         ref.close()

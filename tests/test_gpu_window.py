@@ -109,3 +109,38 @@ def test_window_rejects_due_pulse():
             commit_window(gpu, Operation.create_transfers, [b1, b2], tick_ns=NS_PER_S - 4)
     finally:
         gpu.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,win,bm", [(11, 1, 64), (12, 4, 128), (13, 2, 1024)])
+def test_components_match_sequential_walker(seed, win, bm):
+    """Component-parallel walkers (cpw.h) vs the single sequential walker on chaos streams with
+    limits stripped from the accounts (so that windows qualify): identical replies and stores."""
+    from tigerbeetle_amd import StateMachine
+
+    out = []
+    for components in (True, False):
+        gpu = StateMachine(batch_max=bm, accounts_max=1 << 12, transfers_max=1 << 17, window_events_max=win * bm,
+                           components=components)
+        ch = Chaos(2000 + seed, n_accounts=60, id_space=2000)
+        replies = []
+        try:
+            for w in range(14):
+                if w < 2:
+                    op = Operation.create_accounts
+                    batches = [ch.accounts_batch(ch.rng.randint(1, bm)) for _ in range(win)]
+                    for b in batches:
+                        b["flags"] &= ~np.uint16(6)  # no balance limits
+                else:
+                    op = Operation.create_transfers
+                    batches = [ch.transfers_batch(ch.rng.choice([1, 3, bm // 2, bm])) for _ in range(win)]
+                    for b in batches:
+                        b["flags"] &= ~np.uint16(0x30)  # no balancing
+                replies.append(commit_window(gpu, op, batches, NS_PER_S))
+            st = gpu.stats()
+            out.append((replies, gpu.dump_accounts().tobytes(), gpu.dump_transfers().tobytes(), st))
+        finally:
+            gpu.close()
+    assert out[0][0] == out[1][0]
+    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
+    assert out[0][3]["component_events"] > 0 and out[1][3]["component_events"] == 0

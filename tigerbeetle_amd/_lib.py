@@ -15,7 +15,7 @@ EXPORTS = [
     "tbg_dump_accounts", "tbg_dump_transfers", "tbg_dump_transfer_status", "tbg_device_stores",
     "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_version", "tbg_debug_last_batch",
     "tbg_timing_enable", "tbg_timing_collect", "tbg_gen_accounts_cfg3", "tbg_gen_funding_cfg3",
-    "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4",
+    "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4", "tbg_debug_counters",
 ]
 
 
@@ -34,13 +34,14 @@ class Config(ctypes.Structure):
 
 
 FLAG_NO_RESOLVER = 1
+FLAG_NO_COMPONENTS = 2
 
 
 class Stats(ctypes.Structure):
     _fields_ = [("accounts", ctypes.c_uint64), ("transfers", ctypes.c_uint64),
                 ("expiry_entries", ctypes.c_uint64), ("pulse_next_timestamp", ctypes.c_uint64),
                 ("events_total", ctypes.c_uint64), ("walker_events", ctypes.c_uint64),
-                ("resolver_events", ctypes.c_uint64)]
+                ("resolver_events", ctypes.c_uint64), ("component_events", ctypes.c_uint64)]
 
 
 _lib = None
@@ -89,6 +90,7 @@ def lib():
         "tbg_gen_funding_cfg3": ([vp, u64, u64, u64, u64, u64, u64, u64, vp], i32),
         "tbg_gen_transfers_zipf": ([vp, u64, u64, u64, u64, vp, u64, vp], i32),
         "tbg_gen_transfers_cfg4": ([vp, u64, u64, u64, u64, u64, u64, vp], i32),
+        "tbg_debug_counters": ([vp, vp, u32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -1,0 +1,106 @@
+// cpw.h — component-parallel walking of W (windows where no decision reads a balance).
+//
+// When no event of the window reads an account balance (no hot account: no limit flag and no
+// balancing among the events that reach the balance checks) and the window is overflow-free, the
+// only order dependences between W events are through
+//   - linked chains (consecutive events, state_machine.zig:1236-1300),
+//   - transfer ids: duplicate ids (the exists check, :1487-1490) and pending ids (post/void of a
+//     pending transfer created in the window or posted/voided several times, :1616-1680).
+// Those links partition W into connected components that are mutually independent: the reference's
+// sequential loop restricted to one component yields the same outcomes as the whole loop. Balance
+// effects are commutative adds (nothing reads them), applied atomically.
+//
+// So: union-find over the links (events as nodes; a key's first claimant in the window key map
+// stands for the key), a stable sort of W by component root (window order inside a component is
+// kept), then one walker thread per component (walker.h in atomic-balance mode, with a private undo
+// region). The window's sequential walker is skipped; k_walk only folds the outcomes.
+#pragma once
+#include "walker.h"
+
+__device__ inline bool cpw_active(const Globals* g) { return !g->hot_count && !window_ovf_mode(g); }
+
+__device__ inline uint32_t cc_find(const uint32_t* parent, uint32_t x) {
+  for (;;) {
+    const uint32_t p = __hip_atomic_load(&parent[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p == x) return x;
+    x = p;
+  }
+}
+
+// Hooks the larger root under the smaller one (CAS on the root's parent word; retries on races).
+__device__ inline void cc_union(uint32_t* parent, uint32_t a, uint32_t b) {
+  for (;;) {
+    a = cc_find(parent, a);
+    b = cc_find(parent, b);
+    if (a == b) return;
+    if (a < b) {
+      const uint32_t t = a;
+      a = b;
+      b = t;
+    }
+    if (atomicCAS(&parent[a], a, b) == a) return;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_cc_init(Dev d, Scratch s, uint32_t E) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) d.g->cc_count = 0;
+  if (i >= E || !cpw_active(d.g)) return;
+  s.cc_parent[i] = i;
+}
+
+__global__ void __launch_bounds__(256) k_cc_link(Dev d, Scratch s, WinDesc w, uint32_t epoch) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w.E || !cpw_active(d.g)) return;
+  const uint32_t cls = s.cls[i];
+  if (!(cls & C_W)) return;
+  if ((cls & C_LINKED) && i + 1 < w.off[s.batch[i] + 1]) cc_union(s.cc_parent, i, i + 1);
+  if (!(cls & C_REACH)) return;
+  const uint64_t k = s.bmap[s.id_ent[i]].key;
+  if (bk_epoch(k) == epoch && bk_owner(k) != i) cc_union(s.cc_parent, i, bk_owner(k));
+  if (cls & C_POSTVOID) {
+    const uint64_t kp = s.bmap[s.pid_ent[i]].key;
+    if (bk_epoch(kp) == epoch && bk_owner(kp) != i) cc_union(s.cc_parent, i, bk_owner(kp));
+  }
+}
+
+// Sort keys: the component root of each W event (others: past the end).
+__global__ void __launch_bounds__(256) k_cc_keys(Dev d, Scratch s, uint32_t E) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E) return;
+  const bool on = cpw_active(d.g) && (s.cls[i] & C_W);
+  s.rkey_in[i] = on ? cc_find(s.cc_parent, i) : RES_DUMMY;
+  s.rval_in[i] = i;
+}
+
+// Component starts in the sorted order.
+__global__ void __launch_bounds__(256) k_cc_segs(Dev d, Scratch s, uint32_t E) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= E || !cpw_active(d.g)) return;
+  const uint32_t key = s.rkey[k];
+  if (key == RES_DUMMY || (k > 0 && s.rkey[k - 1] == key)) return;
+  s.cc_list[atomicAdd(&d.g->cc_count, 1u)] = k;
+}
+
+// One walker per component: events rval[start .. start + len), undo records from 5 * start.
+template <bool XFER>
+__global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t* ev, WinDesc w, uint32_t epoch) {
+  Globals* g = d.g;
+  if (!cpw_active(g)) return;
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j == 0) g->cpw_done = 1;
+  if (j >= g->cc_count) return;
+  const uint32_t start = s.cc_list[j];
+  const uint32_t key = s.rkey[start];
+  uint32_t len = 1;
+  while (start + len < w.E && s.rkey[start + len] == key) len++;
+  Walker wk;
+  wk.d = d;
+  wk.s = s;
+  wk.s.undo = s.undo + 5ull * start;
+  wk.ev = ev;
+  wk.w = &w;
+  wk.epoch = epoch;
+  wk.atomic_bal = true;
+  wk.template run<XFER>(s.rval + start, len);
+}

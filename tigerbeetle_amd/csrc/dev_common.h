@@ -101,6 +101,11 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t light_count; // hot ranks walked by one lane
   uint64_t res_events_total;  // cumulative W events decided by the resolver
   uint64_t limited_accounts;  // accounts created with a balance-limit flag (cumulative)
+  uint64_t dbg[8];            // resolver instrumentation (tbg_debug_counters)
+  // component-parallel walker (cpw.h), per window; reset by k_final's last event
+  uint32_t cc_count;    // components of W
+  uint32_t cpw_done;    // the component walkers decided every W event
+  uint64_t cpw_events_total;  // cumulative W events decided by component walkers
 };
 
 // Per-event class bits (scratch `cls`).

@@ -394,6 +394,8 @@ __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, u
   if (XFER && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(&d.g->res_inelig, 1u);
 }
 
+#include "cpw.h"
+
 // ------------------------------------------------------------------------------------------------
 // Segment counts and the ordered W list (one event per thread, one 1024-event segment per block).
 // ------------------------------------------------------------------------------------------------
@@ -447,22 +449,34 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
   for (uint32_t j = threadIdx.x; j < nseg; j += WALK_THREADS) v += s.cnt_w[j];
   const uint32_t w_count = block_sum<WALK_THREADS / 64>(v, lds);
   if (w_count == 0) {
-    if (threadIdx.x == 0) d.g->events_total += w.E;
+    if (threadIdx.x == 0) {
+      d.g->events_total += w.E;
+      d.g->w_count = 0;
+    }
     return;
   }
-  const bool resolved = XFER && d.g->res_done;  // resolver.h decided every W event
-  if (threadIdx.x == 0 && resolved) {
-    d.g->res_events_total += w_count;
+  if (threadIdx.x == 0) d.g->w_count = w_count;
+  if (XFER && d.g->res_done) {
+    // resolver.h decided every W event and folded them into the segment counts
+    if (threadIdx.x == 0) {
+      d.g->res_events_total += w_count;
+      d.g->events_total += w.E;
+    }
+    return;
+  }
+  if (threadIdx.x == 0 && d.g->cpw_done) {  // cpw.h walked W; fold below
+    d.g->cpw_events_total += w_count;
     d.g->events_total += w.E;
   }
-  if (threadIdx.x == 0 && !resolved) {
+  if (threadIdx.x == 0 && !d.g->cpw_done) {
     Walker wk;
     wk.d = d;
     wk.s = s;
     wk.ev = ev;
     wk.w = &w;
     wk.epoch = epoch;
-    wk.template run<XFER>(w_count);
+    wk.atomic_bal = false;
+    wk.template run<XFER>(s.wlist, w_count);
     d.g->w_events_total += w_count;
     d.g->events_total += w.E;
   }
@@ -644,6 +658,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     gw->res_done = 0;
     gw->heavy_count = 0;
     gw->light_count = 0;
+    gw->cpw_done = 0;
   }
 }
 

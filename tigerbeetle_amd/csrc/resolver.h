@@ -39,7 +39,7 @@
 
 #define RES_KEY_BITS 21
 #define RES_DUMMY ((1u << RES_KEY_BITS) - 1)
-#define HEAVY_T 64
+#define HEAVY_T 16
 
 enum : uint32_t { ST_DR_KNOWN = 1, ST_DR_PASS = 2, ST_CR_KNOWN = 4, ST_CR_PASS = 8 };
 // entry meta: [19:0] event | side | check (this side reads A) | wait (the other side reads) |
@@ -176,7 +176,19 @@ __device__ inline u128 u128_wave_sum(u128 v) {
 }
 
 #define RES_THREADS 256
+#ifndef RES_DBG
+#define RES_DBG 0  // 1: count steps / blocks / spin time into Globals::dbg (tbg_debug_counters)
+#endif
+#define DBG_ADD(k, v) \
+  do {                                                                             \
+    if (RES_DBG) atomicAdd((unsigned long long*)&g->dbg[k], (unsigned long long)(v)); \
+  } while (0)
+#define DBG_MAX(k, v) \
+  do {                                                                             \
+    if (RES_DBG) atomicMax((unsigned long long*)&g->dbg[k], (unsigned long long)(v)); \
+  } while (0)
 #define RES_BUDGET 32
+#define RES_LANE_BUDGET 8
 #define RES_TIMEOUT_TICKS 20000000ull  // 200 ms of s_memrealtime (100 MHz) without progress
 
 // Gives up (all waves) once any wave has waited RES_TIMEOUT_TICKS without progress.
@@ -202,30 +214,38 @@ __device__ inline bool wave_advance(Globals* g, const Scratch& s, uint32_t r, bo
   const uint32_t pos0 = pos;
   u128 acc[4] = {0, 0, 0, 0};
   uint64_t last = wall_clock64();
+  // entries of the current step, loaded one step ahead
+  uint32_t meta = 0;
+  __int128 amt = 0;
+  if (start + pos + lane < end) {
+    meta = s.rmeta[start + pos + lane];
+    amt = (__int128)s.ramt[start + pos + lane];
+  }
   for (uint32_t step = 0; (exclusive || step < budget) && start + pos < end; step++) {
     const uint32_t k0 = start + pos;
     const uint32_t n = min(64u, end - k0);
     const bool act = (uint32_t)lane < n;
-    uint32_t meta = 0;
-    __int128 amt = 0;
-    if (act) {
-      meta = s.rmeta[k0 + lane];
-      amt = (__int128)s.ramt[k0 + lane];
-    }
     const uint32_t e = meta & RM_EVENT;
     const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
     const bool check = meta & RM_CHECK;
     bool have = true, opass = true;
+    uint32_t w = 0;
+    if (act && (meta & RM_WAIT)) w = st_load(&s.st[e]);
+    // prefetch the next step's entries (used if this step is not blocked)
+    uint32_t meta_n = 0;
+    __int128 amt_n = 0;
+    if (k0 + 64 + lane < end) {
+      meta_n = s.rmeta[k0 + 64 + lane];
+      amt_n = (__int128)s.ramt[k0 + 64 + lane];
+    }
     if (act && (meta & RM_WAIT)) {
-      const uint32_t w = st_load(&s.st[e]);
       have = w & st_known(side ^ 1);
       opass = w & (side ? ST_DR_PASS : ST_CR_PASS);
     }
     const unsigned long long blocked = __ballot(act && !have);
     const uint32_t lim = blocked ? (uint32_t)__builtin_ctzll(blocked) : n;
-    const bool in = (uint32_t)lane < lim;
     // effects on A assuming every check passes
-    bool ok = in && opass;
+    bool ok = (uint32_t)lane < lim && opass;
     __int128 eff = 0;
     if (ok) eff = check ? -amt : ((meta & RM_ADD) ? amt : (__int128)0);
     __int128 x = eff;
@@ -261,17 +281,30 @@ __device__ inline bool wave_advance(Globals* g, const Scratch& s, uint32_t r, bo
     }
     if (lim > 0) A = i128_shfl(P + eff, (int)lim - 1);
     pos += lim;
-    if (lim < n) {
+    if (lane == 0) DBG_ADD(0, 1);
+    if (lim == n) {
+      meta = meta_n;
+      amt = amt_n;
+    } else {
+      if (lane == 0) DBG_ADD(1, 1);
       if (!exclusive) break;
       // wait for the blocking lane's other side, then redo the step from there
       const uint32_t eb = (uint32_t)__shfl((int)e, (int)lim, 64);
       const uint32_t sb = (uint32_t)__shfl((int)side, (int)lim, 64);
       if (lim > 0) last = wall_clock64();
+      const uint64_t t_spin = wall_clock64();
       while (!(st_load(&s.st[eb]) & st_known(sb ^ 1))) {
         if (res_stalled(g, last)) return false;
         __builtin_amdgcn_s_sleep(1);
       }
       last = wall_clock64();
+      if (lane == 0) DBG_ADD(2, last - t_spin);
+      meta = 0;
+      amt = 0;
+      if (start + pos + lane < end) {
+        meta = s.rmeta[start + pos + lane];
+        amt = (__int128)s.ramt[start + pos + lane];
+      }
     }
   }
 #pragma unroll
@@ -297,10 +330,20 @@ __device__ inline bool lane_advance(const Scratch& s, uint32_t r, uint32_t budge
   const uint32_t pos0 = pos;
   __int128 A = rsp->A;
   u128 d0 = rsp->d[0], d1 = rsp->d[1], d2 = rsp->d[2], d3 = rsp->d[3];
+  uint32_t meta_n = 0;
+  __int128 amt_n = 0;
+  if (start + pos < end) {
+    meta_n = s.rmeta[start + pos];
+    amt_n = (__int128)s.ramt[start + pos];
+  }
   for (uint32_t step = 0; step < budget && start + pos < end; step++) {
     const uint32_t k = start + pos;
-    const uint32_t meta = s.rmeta[k];
-    const __int128 amt = (__int128)s.ramt[k];
+    const uint32_t meta = meta_n;
+    const __int128 amt = amt_n;
+    if (k + 1 < end) {
+      meta_n = s.rmeta[k + 1];
+      amt_n = (__int128)s.ramt[k + 1];
+    }
     const uint32_t e = meta & RM_EVENT;
     const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
     const bool check = meta & RM_CHECK;
@@ -354,7 +397,12 @@ __global__ void __launch_bounds__(RES_THREADS) k_res_walk(Dev d, Scratch s) {
   const uint32_t wave = blockIdx.x * (RES_THREADS / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const uint32_t Ph = min(H, L ? P / 2 : P);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    DBG_ADD(5, H);
+    DBG_ADD(6, L);
+  }
   uint64_t last = wall_clock64();
+  const uint64_t t_begin = last;
   if (wave < Ph) {
     const bool exclusive = H <= Ph;
     for (;;) {
@@ -368,7 +416,10 @@ __global__ void __launch_bounds__(RES_THREADS) k_res_walk(Dev d, Scratch s) {
         any_moved |= moved;
         any_left |= !done;
       }
-      if (!any_left) return;
+      if (!any_left) {
+        if (lane == 0) DBG_MAX(3, wall_clock64() - t_begin);
+        return;
+      }
       if (any_moved) {
         last = wall_clock64();
       } else {
@@ -387,11 +438,15 @@ __global__ void __launch_bounds__(RES_THREADS) k_res_walk(Dev d, Scratch s) {
       const RState* rsp = &s.rstate[r];
       if (rsp->start + rsp->pos >= rsp->end) continue;
       bool done = false;
-      if (lane_advance(s, r, RES_BUDGET, &done)) moved = true;
+      if (lane_advance(s, r, RES_LANE_BUDGET, &done)) moved = true;
       if (!done) left = true;
     }
     const bool any_left = __any(left), any_moved = __any(moved);
-    if (!any_left) return;
+    if (lane == 0) DBG_ADD(7, 1);
+    if (!any_left) {
+      if (lane == 0) DBG_MAX(4, wall_clock64() - t_begin);
+      return;
+    }
     if (any_moved) {
       last = wall_clock64();
     } else {
@@ -415,31 +470,43 @@ __global__ void __launch_bounds__(256) k_res_apply(Dev d, Scratch s) {
   a.credits_posted = W(U(a.credits_posted) + rs.d[3]);
 }
 
-// Final outcomes of the W events from the published checks (unless a wave gave up).
+// Final outcomes of the W events from the published checks (unless a wave gave up), folded into
+// the per-segment failure / insert counts (a 256-event block lies inside one 1024-event segment).
 __global__ void __launch_bounds__(256) k_res_final(Dev d, Scratch s, uint32_t E, uint32_t epoch) {
+  __shared__ uint32_t nbad, nins;
   Globals* g = d.g;
   if (g->res_inelig || !g->hot_count || g->res_error) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) g->res_done = 1;
-  if (i >= E) return;
-  uint32_t cls = s.cls[i];
-  if (!(cls & C_W)) return;
-  uint32_t code = s.code[i];
-  if (code == TB_CT_OK && (cls & (C_READS_DR | C_READS_CR))) {
-    const uint32_t w = s.st[i];
-    if ((cls & C_READS_DR) && !(w & ST_DR_PASS))
-      code = TB_CT_EXCEEDS_CREDITS;
-    else if ((cls & C_READS_CR) && !(w & ST_CR_PASS))
-      code = TB_CT_EXCEEDS_DEBITS;
-    s.code[i] = code;
+  if (threadIdx.x == 0) nbad = nins = 0;
+  __syncthreads();
+  uint32_t cls = i < E ? s.cls[i] : 0u;
+  if (cls & C_W) {
+    uint32_t code = s.code[i];
+    if (code == TB_CT_OK && (cls & (C_READS_DR | C_READS_CR))) {
+      const uint32_t w = s.st[i];
+      if ((cls & C_READS_DR) && !(w & ST_DR_PASS))
+        code = TB_CT_EXCEEDS_CREDITS;
+      else if ((cls & C_READS_CR) && !(w & ST_CR_PASS))
+        code = TB_CT_EXCEEDS_DEBITS;
+      s.code[i] = code;
+    }
+    const bool ok = code == TB_CT_OK;
+    const bool ins = ok && (cls & C_INSERT);
+    s.ins[i] = ins ? 1 : 0;
+    cls = (cls & ~C_W) | (ok ? C_COMMIT : 0u) | (ins ? C_INSERTED : 0u);
+    if (ok) {
+      if (d.hot[s.dr_slot[i]] == epoch) cls |= C_RES_DR;
+      if (d.hot[s.cr_slot[i]] == epoch) cls |= C_RES_CR;
+    }
+    s.cls[i] = cls;
+    if (!ok) atomicAdd(&nbad, 1u);
+    if (ins) atomicAdd(&nins, 1u);
   }
-  const bool ok = code == TB_CT_OK;
-  const bool ins = ok && (cls & C_INSERT);
-  s.ins[i] = ins ? 1 : 0;
-  cls = (cls & ~C_W) | (ok ? C_COMMIT : 0u) | (ins ? C_INSERTED : 0u);
-  if (ok) {
-    if (d.hot[s.dr_slot[i]] == epoch) cls |= C_RES_DR;
-    if (d.hot[s.cr_slot[i]] == epoch) cls |= C_RES_CR;
+  __syncthreads();
+  if (threadIdx.x == 0 && (nbad | nins)) {
+    const uint32_t seg = (blockIdx.x * blockDim.x) / SEG;
+    if (nbad) atomicAdd(&s.cnt_bad[seg], nbad);
+    if (nins) atomicAdd(&s.cnt_ins[seg], nins);
   }
-  s.cls[i] = cls;
 }

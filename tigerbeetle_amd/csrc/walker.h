@@ -62,6 +62,11 @@ struct Walker {
   uint32_t epoch;
   uint32_t undo_n;
   bool scope;
+  // Component-parallel mode (k_cc_walk): other walkers run concurrently on other components and may
+  // touch the same accounts, so balance effects are atomic adds (undone by atomic subtracts). Only
+  // used in windows where no decision reads a balance (no hot account, no overflow risk), so the
+  // racy balance values read below never change an outcome.
+  bool atomic_bal;
 
   __device__ void log_bal(uint32_t slot) {
     if (!scope) return;
@@ -81,10 +86,23 @@ struct Walker {
     r.a = a;
     r.old[0] = old;
   }
+  __device__ static tb_uint128_t* bal_field(tb_account_t* a, uint32_t f) {
+    return f == 0 ? &a->debits_pending : f == 1 ? &a->debits_posted : f == 2 ? &a->credits_pending : &a->credits_posted;
+  }
+  __device__ void add_bal(uint32_t slot, uint32_t f, u128 v) {
+    atomic_add_u128(bal_field(&d.acc[slot], f), v);
+    if (!scope) return;
+    UndoRec& r = s.undo[undo_n++];
+    r.kind = UNDO_ADD;
+    r.a = slot;
+    r.pad0 = f;
+    r.old[0] = v;
+  }
   __device__ void rollback() {
     while (undo_n) {
       const UndoRec& r = s.undo[--undo_n];
       switch (r.kind) {
+        case UNDO_ADD: atomic_add_u128(bal_field(&d.acc[r.a], r.pad0), (u128)0 - r.old[0]); break;
         case UNDO_BAL: {
           Bal b;
           b.dp = r.old[0];
@@ -128,6 +146,13 @@ struct Walker {
     if (r != TB_CT_OK) return r;
     t.amount = W(amount);
     commit_record(i, t);
+    if (atomic_bal) {
+      const bool pend = t.flags & TB_TRANSFER_PENDING;
+      add_bal(drs, pend ? 0 : 1, amount);
+      add_bal(crs, pend ? 2 : 3, amount);
+      if (pend) s.bstatus[i] = TB_PENDING_PENDING;
+      return TB_CT_OK;
+    }
     log_bal(drs);
     log_bal(crs);
     if (t.flags & TB_TRANSFER_PENDING) {
@@ -178,12 +203,21 @@ struct Walker {
       log_small(UNDO_XST, pslot, d.xstatus[pslot]);
       d.xstatus[pslot] = st;
     }
+    const u128 pa = U(p.amount);
+    if (atomic_bal) {
+      add_bal(drs, 0, (u128)0 - pa);
+      add_bal(crs, 2, (u128)0 - pa);
+      if (t.flags & TB_TRANSFER_POST_PENDING) {
+        add_bal(drs, 1, amount);
+        add_bal(crs, 3, amount);
+      }
+      return TB_CT_OK;
+    }
     tb_account_t* dra = &d.acc[drs];
     tb_account_t* cra = &d.acc[crs];
     Bal dr = load_bal(dra), cr = load_bal(cra);
     log_bal(drs);
     log_bal(crs);
-    const u128 pa = U(p.amount);
     dr.dp -= pa;
     cr.cp -= pa;
     if (t.flags & TB_TRANSFER_POST_PENDING) {
@@ -210,14 +244,15 @@ struct Walker {
     return TB_CA_OK;
   }
 
+  // Walks the events list[0..count) (ascending window positions).
   template <bool XFER>
-  __device__ void run(uint32_t w_count) {
+  __device__ void run(const uint32_t* list, uint32_t count) {
     int32_t chain = -1;
     bool broken = false;
     undo_n = 0;
     scope = false;
-    for (uint32_t k = 0; k < w_count; k++) {
-      const uint32_t i = s.wlist[k];
+    for (uint32_t k = 0; k < count; k++) {
+      const uint32_t i = list[k];
       const uint32_t cls = s.cls[i];
       const bool linked = cls & C_LINKED;
       const uint32_t b = s.batch[i];

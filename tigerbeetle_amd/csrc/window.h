@@ -33,7 +33,7 @@ __device__ inline uint64_t win_ts(const WinDesc& w, uint32_t b, uint32_t i) {
   return w.T[b] - n + (i - w.off[b]) + 1;
 }
 
-enum : uint32_t { UNDO_BAL = 1, UNDO_XST, UNDO_BST, UNDO_COMMIT, UNDO_INS };
+enum : uint32_t { UNDO_BAL = 1, UNDO_XST, UNDO_BST, UNDO_COMMIT, UNDO_INS, UNDO_ADD };
 struct __attribute__((aligned(16))) UndoRec {
   uint32_t kind, a, pad0, pad1;
   u128 old[4];
@@ -72,6 +72,7 @@ struct Scratch {
   struct RState* rstate;                      // per hot rank: segment, cursor, available balance
   uint32_t* st;                               // per event: published limit-check outcomes
   uint32_t *heavy, *light;                    // hot ranks by walker kind
+  uint32_t *cc_parent, *cc_list;              // component-parallel walker (cpw.h)
   void* sort_tmp;
   size_t sort_tmp_bytes;
 };
