@@ -32,6 +32,8 @@ typedef struct tbg_config {
     uint64_t transfers_max;  /* capacity of the transfer store */
     uint32_t window_events_max; /* events per commit window (tbg_commit_window); 0 = batch_max */
     uint32_t flags;          /* TBG_FLAG_* */
+    uint32_t shard_count;    /* 0: unsharded engine; G >= 1: this engine is one of G hash shards */
+    uint32_t shard_index;    /* this engine's shard, < shard_count */
 } tbg_config;
 
 /* Decide balance-limit windows on the sequential walker only (no account-parallel resolver). */
@@ -44,6 +46,7 @@ typedef struct tbg_config {
 #define TBG_E_CAPACITY (-2)  /* store capacity exceeded (no state changed) */
 #define TBG_E_DEVICE (-3)    /* HIP runtime / device failure: fatal */
 #define TBG_E_STATE (-4)     /* API misuse (e.g. commit timestamp not increasing) */
+#define TBG_E_UNSUPPORTED (-5) /* sharded engine: a window outside the sharded class (nothing applied) */
 
 /* StateMachine.init (state_machine.zig:455-477) / deinit (:479-484). */
 int tbg_create(const tbg_config *config, tbg_engine **out);
@@ -92,6 +95,24 @@ int tbg_commit_window(tbg_engine *engine, uint32_t operation, const void *d_even
 int tbg_sync(tbg_engine *engine);
 /* The engine's HIP stream (hipStream_t), for callers that time or order around it. */
 void *tbg_stream(tbg_engine *engine);
+
+/* Hash-sharded commit over G GPUs of one node (tigerbeetle_amd/csrc/shard.h). The replacement for
+ * the same commit (state_machine.zig:1220-1306) when accounts are partitioned across engines:
+ * account a lives on shard tbg_shard_of(a.id), transfer t on shard tbg_shard_of(t.id). Every shard
+ * receives the same window (same arguments as tbg_commit_window) and:
+ *   1. tbg_shard_prepare_window: validates, resolves what it owns, writes (E + 1) x 16 B int32 words
+ *      at d_exchange (word 0 = trailer, word 1 + i = event i);
+ *   2. the caller sums d_exchange element-wise across all G shards in place, ordered on the engine
+ *      stream (ncclAllReduce(int32, ncclSum) over xGMI, e.g. torch.distributed.all_reduce);
+ *   3. tbg_shard_commit_window: decides every event identically on every shard, writes the window's
+ *      replies (as tbg_commit_window) and applies only the owned effects.
+ * Sharded class: create_accounts and create_transfers without limits, balancing, two-phase or
+ * in-window duplicate ids, overflow-free. Any other window is rejected whole on every shard:
+ * tbg_sync returns TBG_E_UNSUPPORTED and no shard has applied it. Asynchronous on the engine stream. */
+uint32_t tbg_shard_of(uint64_t id_lo, uint64_t id_hi, uint32_t shard_count);
+int tbg_shard_prepare_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_batches,
+                             const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_exchange);
+int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, void *d_results, uint32_t *d_batch_base);
 
 /* Test hook mirroring the harness `setup` action (state_machine.zig:2545-2561). */
 int tbg_setup_balances(tbg_engine *engine, const tb_uint128_t *id, const tb_uint128_t *debits_pending,

@@ -15,7 +15,8 @@ EXPORTS = [
     "tbg_dump_accounts", "tbg_dump_transfers", "tbg_dump_transfer_status", "tbg_device_stores",
     "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_version", "tbg_debug_last_batch",
     "tbg_timing_enable", "tbg_timing_collect", "tbg_gen_accounts_cfg3", "tbg_gen_funding_cfg3",
-    "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4", "tbg_debug_counters",
+    "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4", "tbg_debug_counters", "tbg_shard_of",
+    "tbg_shard_prepare_window", "tbg_shard_commit_window",
 ]
 
 
@@ -30,7 +31,8 @@ def u128(v):
 class Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("batch_max", ctypes.c_uint32),
                 ("accounts_max", ctypes.c_uint64), ("transfers_max", ctypes.c_uint64),
-                ("window_events_max", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+                ("window_events_max", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("shard_count", ctypes.c_uint32), ("shard_index", ctypes.c_uint32)]
 
 
 FLAG_NO_RESOLVER = 1
@@ -91,6 +93,9 @@ def lib():
         "tbg_gen_transfers_zipf": ([vp, u64, u64, u64, u64, vp, u64, vp], i32),
         "tbg_gen_transfers_cfg4": ([vp, u64, u64, u64, u64, u64, u64, vp], i32),
         "tbg_debug_counters": ([vp, vp, u32], i32),
+        "tbg_shard_of": ([u64, u64, u32], u32),
+        "tbg_shard_prepare_window": ([vp, u32, vp, u32, vp, vp, vp], i32),
+        "tbg_shard_commit_window": ([vp, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -100,6 +105,15 @@ def lib():
     return L
 
 
+E_UNSUPPORTED = -5
+
+
+class UnsupportedWindow(RuntimeError):
+    """A sharded engine rejected a window outside its class (nothing was applied)."""
+
+
 def check(rc, what):
+    if rc == E_UNSUPPORTED:
+        raise UnsupportedWindow(f"{what}: window outside the sharded class (status {rc})")
     if rc != 0:
         raise RuntimeError(f"{what} failed with status {rc}")

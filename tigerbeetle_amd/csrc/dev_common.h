@@ -106,6 +106,10 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t cc_count;    // components of W
   uint32_t cpw_done;    // the component walkers decided every W event
   uint64_t cpw_events_total;  // cumulative W events decided by component walkers
+  // sharded engines (shard.h), per window
+  uint32_t sh_blocks;   // prep blocks finished (the last one closes the trailer word)
+  uint32_t sh_unsup;    // the window is outside the sharded class: nothing is applied
+  uint64_t sh_own;      // events this shard owns the id of (capacity check)
 };
 
 // Per-event class bits (scratch `cls`).
@@ -128,6 +132,7 @@ enum : uint32_t {
   C_BAL = 1u << 15,        // balancing_debit or balancing_credit
   C_RES_DR = 1u << 16,     // final: the resolver applied this event's debit-account effects
   C_RES_CR = 1u << 17,     // final: the resolver applied this event's credit-account effects
+  C_OWN = 1u << 18,        // sharded: this shard owns the event's id (it inserts the record)
 };
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

@@ -662,6 +662,8 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   }
 }
 
+#include "shard.h"
+
 // ------------------------------------------------------------------------------------------------
 // Pulse: ExpirePendingTransfers scan + execute_expire_pending_transfers (state_machine.zig:
 // 1010-1105, 1874-1929, 2112-2166). The live list holds scan-visible pending-with-timeout entries;

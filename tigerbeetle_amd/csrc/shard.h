@@ -1,0 +1,405 @@
+// shard.h — hash-sharded commit across G GPUs of one node (one engine per GPU).
+//
+// Ownership: an account belongs to shard_of(account id), a transfer to shard_of(transfer id). Every
+// shard holds the whole prepared window in HBM (the replica hands each GPU the same prepare body)
+// and walks all of it, but touches state only for what it owns:
+//
+//   k_sh_prep    grid   stateless validation (identical on every shard, state_machine.zig:1424-1439,
+//                       1465-1489); for each event that passes, the debit-account owner resolves the
+//                       debit account, the credit-account owner the credit account, the transfer-id
+//                       owner the id (pre-window `exists` comparison, :1506-1507, and in-window
+//                       duplicates through the window key map). Each writes its part of the event's
+//                       16 B exchange word; the other parts stay zero.
+//   (caller)            sum-all-reduce of the exchange words across the shards (RCCL over xGMI). Each
+//                       field has exactly one writer, so the sum is the union of the owners' parts.
+//   k_sh_decide  grid   every shard now holds the same per-event facts and decides every event the
+//                       same way: account lookups (:1496-1497), ledgers (:1503-1504), exists, then
+//                       linked chains (:1240-1300); identical replies on all shards.
+//   k_wcount     grid   per-segment failure / owned-insert counts.
+//   k_sh_final   grid   replies, and only owned effects: the id owner appends the record and indexes the
+//                       id, the debit/credit owners add the amount (exact 128-bit atomics).
+//
+// The sharded class is the order-free one: no balance read (no limit flag on a touched
+// account, no balancing), no two-phase, no in-window duplicate id, overflow-free window. Then every
+// event's outcome is a function of the owners' facts alone, and the effects commute. A window outside
+// the class is detected before anything is applied, identically on every shard (its flags travel in
+// the exchange's trailer word or follow from the reduced words), and fails with TBG_E_UNSUPPORTED at
+// tbg_sync: no shard applies any of it.
+#pragma once
+#include "sm_logic.h"
+#include "walker.h"
+#include "window.h"
+
+// Exchange word per event (summed over shards; one writer per field):
+//   x: debit account's ledger (its owner; 0 = not found: an account's ledger is never 0, :1436)
+//   y: credit account's ledger
+//   z: transfer-id owner: 1 + (TB_CT_OK or the exists* code); create_accounts: 1 + the owner's code
+//   w: bit 0 debit account has debits_must_not_exceed_credits, bit 1 credit account has
+//      credits_must_not_exceed_debits (balance reads: outside the sharded class)
+// Word 0 is the trailer: x = shards that saw an unsupported event, y = shards over capacity,
+// z = shards whose overflow bound does not clear the window's amounts.
+enum : uint32_t { SH_W_DR_LIMIT = 1, SH_W_CR_LIMIT = 2 };
+
+// Guard on every computed index of the sharded path: a violation is recorded (first one wins:
+// check id << 48 | shard-local value, in Globals::dbg[7]), the window is failed as a device error
+// (window_error bit 2) and the access is skipped. Never expected to fire.
+__device__ inline bool sh_guard(Globals* g, bool ok, uint32_t check, uint64_t value) {
+  if (ok) return true;
+  atomicCAS(reinterpret_cast<unsigned long long*>(&g->dbg[7]), 0ull,
+            ((unsigned long long)check << 48) | (value & 0xFFFFFFFFFFFFull));
+  atomicOr(&g->window_error, 4u);
+  return false;
+}
+
+// Owner of an id among G shards: the high half of the table hash (the tables index with the low
+// bits, so a shard's own keys still spread over its whole table).
+__host__ __device__ inline uint32_t shard_of(uint64_t lo, uint64_t hi, uint32_t G) {
+  return (uint32_t)(((hash_id(lo, hi) >> 32) * (uint64_t)G) >> 32);
+}
+
+// Window key-map claim for the sharded path: returns the entry and whether the key was already
+// claimed in this window (an in-window duplicate id).
+__device__ inline uint32_t sh_claim(Globals* g, BEntry* bm, uint32_t mask, const uint8_t* ev, tb_uint128_t key,
+                                    uint32_t idx, uint32_t E, uint32_t epoch, bool* dup) {
+  const unsigned long long inc = 1ull << 21;
+  uint32_t h = (uint32_t)hash_id(key.lo, key.hi) & mask;
+  for (;;) {
+    unsigned long long old = __hip_atomic_load(&bm[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if (bk_epoch(old) != epoch) {
+        const unsigned long long fresh = ((unsigned long long)epoch << 32) | idx | inc;
+        const unsigned long long prev = atomicCAS(&bm[h].key, old, fresh);
+        if (prev == old) {
+          *dup = false;
+          return h;
+        }
+        old = prev;
+        continue;
+      }
+      if (!sh_guard(g, bk_owner(old) < E && !bk_is_pid(old), 1, old)) {
+        *dup = true;
+        return h;
+      }
+      const tb_uint128_t k = bkey(ev, bk_owner(old), bk_is_pid(old));
+      if (k.lo != key.lo || k.hi != key.hi) break;  // another key: probe on
+      *dup = true;
+      return h;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+// End-of-window device state (the last event's thread of k_sh_final).
+__device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bool apply) {
+  if (apply) {
+    if (xfer) {
+      g->x_count = count;
+      const u128 sum = g->ovf_bound + g->batch_amount_sum;
+      g->ovf_bound = (g->batch_huge || sum < g->ovf_bound) ? MAX128 : sum;
+    } else {
+      g->acc_count = count;
+    }
+  }
+  g->batch_amount_sum = 0;
+  g->batch_huge = 0;
+  g->sh_unsup = 0;
+}
+
+// The last block of a prep launch (after every block's atomics are visible) closes the window's
+// local facts into the trailer word: capacity and overflow verdicts.
+__device__ inline void sh_prep_close(Dev d, uint4* xch, bool xfer) {
+  Globals* g = d.g;
+  __threadfence();
+  const uint32_t done = atomicAdd(&g->sh_blocks, 1u);
+  if (done != gridDim.x - 1) return;
+  __threadfence();
+  g->sh_blocks = 0;
+  const uint64_t own = __hip_atomic_load(&g->sh_own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  g->sh_own = 0;
+  if (xfer) {
+    if (g->x_count + own > d.x_max) xch[0].y = 1;
+    if (window_ovf_mode(g)) xch[0].z = 1;
+  } else {
+    if (g->acc_count + own > d.acc_max) xch[0].y = 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// create_transfers: prep
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
+                                                    uint32_t epoch, uint4* xch, uint32_t G, uint32_t me) {
+  __shared__ u128 red[256];
+  __shared__ uint32_t huge_any, unsup, own;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (threadIdx.x == 0) huge_any = unsup = own = 0;
+  if (i == 0) check_window(w, d.g);
+  __syncthreads();
+  u128 amount_upper = 0;
+  if (i < w.E) {
+    tb_transfer_t t = ev[i];
+    const uint32_t b = win_batch(w, i);
+    uint32_t cls = 0, code, dr_slot = NONE32, cr_slot = NONE32, id_ent = NONE32;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    const uint16_t f = t.flags;
+    if (f & TB_TRANSFER_LINKED) cls |= C_LINKED;
+    if (t.timestamp != 0) {
+      cls |= C_TSNZ;
+      code = TB_CT_TIMESTAMP_MUST_BE_ZERO;
+    } else {
+      t.timestamp = win_ts(w, b, i);
+      code = ct_head(t);
+      if (code == CONT && (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))) {
+        code = pv_validate(t);
+        if (code == CONT) atomicOr(&unsup, 1u);  // two-phase resolution: outside the sharded class
+      } else if (code == CONT) {
+        code = ct_validate(t);
+        if (code == CONT) {
+          if (f & (TB_TRANSFER_PENDING | TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT))
+            atomicOr(&unsup, 1u);
+          cls |= C_REACH;
+          amount_upper = U(t.amount);
+          // up to three independent probes, one per owned side
+          if (shard_of(t.debit_account_id.lo, t.debit_account_id.hi, G) == me) {
+            AccEntry e;
+            dr_slot = acc_find(d.acc_tab, d.acc_mask, t.debit_account_id, &e);
+            if (dr_slot != NONE32) {
+              v.x = e.ledger;
+              if (e.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) v.w |= SH_W_DR_LIMIT;
+            }
+          }
+          if (shard_of(t.credit_account_id.lo, t.credit_account_id.hi, G) == me) {
+            AccEntry e;
+            cr_slot = acc_find(d.acc_tab, d.acc_mask, t.credit_account_id, &e);
+            if (cr_slot != NONE32) {
+              v.y = e.ledger;
+              if (e.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) v.w |= SH_W_CR_LIMIT;
+            }
+          }
+          if (shard_of(t.id.lo, t.id.hi, G) == me) {
+            cls |= C_OWN;
+            atomicAdd(&own, 1u);
+            bool dup;
+            id_ent = sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
+            if (dup) atomicOr(&unsup, 1u);
+            const uint32_t xs = x_find(d.x_tab, d.x_mask, t.id);
+            v.z = 1 + (xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]));
+          }
+        }
+      }
+    }
+    if (code != CONT) cls |= C_STATIC;
+    s.code[i] = code;
+    s.cls[i] = cls;
+    s.batch[i] = (uint16_t)b;
+    s.dr_slot[i] = dr_slot;
+    s.cr_slot[i] = cr_slot;
+    s.id_ent[i] = id_ent;
+    xch[1 + i] = v;
+  }
+  if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&huge_any, 1u);
+  red[threadIdx.x] = ((uint64_t)(amount_upper >> 64) != 0) ? 0 : amount_upper;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (red[0]) atomic_add_u128(reinterpret_cast<tb_uint128_t*>(&d.g->batch_amount_sum), red[0]);
+    if (huge_any) atomicOr(&d.g->batch_huge, 1u);
+    if (unsup) atomicOr(&xch[0].x, 1u);
+    if (own) atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->sh_own), (unsigned long long)own);
+    sh_prep_close(d, xch, true);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// create_accounts: prep
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_sh_prep_ca(Dev d, Scratch s, const tb_account_t* __restrict__ ev, WinDesc w,
+                                                    uint32_t epoch, uint4* xch, uint32_t G, uint32_t me) {
+  __shared__ uint32_t unsup, own;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (threadIdx.x == 0) unsup = own = 0;
+  if (i == 0) check_window(w, d.g);
+  __syncthreads();
+  if (i < w.E) {
+    const tb_account_t a = ev[i];
+    const uint32_t b = win_batch(w, i);
+    uint32_t cls = 0, code, id_ent = NONE32;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (a.flags & TB_ACCOUNT_LINKED) cls |= C_LINKED;
+    if (a.timestamp != 0) {
+      cls |= C_TSNZ;
+      code = TB_CA_TIMESTAMP_MUST_BE_ZERO;
+    } else {
+      code = ca_validate(a);
+      if (code == CONT) {
+        cls |= C_REACH;
+        if (shard_of(a.id.lo, a.id.hi, G) == me) {
+          cls |= C_OWN;
+          atomicAdd(&own, 1u);
+          bool dup;
+          id_ent = sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), a.id, i, w.E, epoch, &dup);
+          if (dup) atomicOr(&unsup, 1u);
+          AccEntry e;
+          const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, a.id, &e);
+          v.z = 1 + (slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(a, d.acc[slot]));
+        }
+      }
+    }
+    if (code != CONT) cls |= C_STATIC;
+    s.code[i] = code;
+    s.cls[i] = cls;
+    s.batch[i] = (uint16_t)b;
+    s.id_ent[i] = id_ent;
+    s.dr_slot[i] = NONE32;
+    s.cr_slot[i] = NONE32;
+    xch[1 + i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (unsup) atomicOr(&xch[0].x, 1u);
+    if (own) atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->sh_own), (unsigned long long)own);
+    sh_prep_close(d, xch, false);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// decide: every shard, every event, from the reduced exchange words.
+// ------------------------------------------------------------------------------------------------
+template <bool XFER>
+__device__ inline uint32_t sh_code(const Dev& d, const Scratch& s, const uint8_t* ev, const uint4* xch, uint32_t j) {
+  const uint32_t code = s.code[j];
+  if (code != CONT) return code;
+  const uint4 v = xch[1 + j];
+  if (!XFER) return v.z - 1;
+  if (v.x == 0) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;  // :1496-1497
+  if (v.y == 0) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
+  if (v.x != v.y) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;  // :1503-1504
+  if (reinterpret_cast<const tb_transfer_t*>(ev)[j].ledger != v.x)
+    return TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+  if (v.z - 1 != TB_CT_OK) return v.z - 1;  // exists* (:1506-1507)
+  // Reaches the balance checks: overflow cannot fail in a class window; a limit flag on either
+  // account is a balance read (:1546-1547), outside the class.
+  if (v.w) atomicOr(&d.g->sh_unsup, 1u);
+  return TB_CT_OK;
+}
+
+template <bool XFER>
+__global__ void __launch_bounds__(256) k_sh_decide(Dev d, Scratch s, const uint8_t* ev, WinDesc w, const uint4* xch) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    const uint4 t = xch[0];
+    if (t.x | t.y | t.z) atomicOr(&d.g->sh_unsup, 1u);
+  }
+  if (i >= w.E) return;
+  const uint32_t b = s.batch[i];
+  const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
+  if (i != first && (s.cls[i - 1] & C_LINKED)) return;  // chain member: its head decides
+  const uint32_t cls = s.cls[i];
+  if (!(cls & C_LINKED)) {
+    const uint32_t code = sh_code<XFER>(d, s, ev, xch, i);
+    s.code[i] = code;
+    if (code == TB_CT_OK) s.cls[i] = cls | C_COMMIT | ((cls & C_OWN) ? C_INSERTED : 0u);
+    return;
+  }
+  // chain head: members i..end (:1240-1300). No member's outcome depends on another member's
+  // effects in a class window, so the chain fails at its first failing member.
+  uint32_t end = i, f = NONE32;
+  for (uint32_t j = i;; j++) {
+    const bool lj = s.cls[j] & C_LINKED;
+    uint32_t code = sh_code<XFER>(d, s, ev, xch, j);
+    if (lj && j == last) code = TB_CT_LINKED_EVENT_CHAIN_OPEN;  // :1247
+    s.code[j] = code;
+    if (code != TB_CT_OK && f == NONE32) f = j;
+    end = j;
+    if (!lj || j == last) break;
+  }
+  for (uint32_t j = i; j <= end; j++) {
+    const uint32_t cj = s.cls[j];
+    if (f == NONE32) {
+      s.cls[j] = cj | C_COMMIT | ((cj & C_OWN) ? C_INSERTED : 0u);
+    } else if (j != f && !((cj & C_LINKED) && j == last)) {
+      s.code[j] = TB_CT_LINKED_EVENT_FAILED;  // back-fill before f, broken chain after f
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// final: replies (every shard) and owned effects.
+// ------------------------------------------------------------------------------------------------
+template <bool XFER>
+__global__ void __launch_bounds__(SEG) k_sh_final(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w, FinalOut o) {
+  __shared__ uint32_t lds[SEG / 64];
+  Globals* g = d.g;
+  const bool unsup = __hip_atomic_load(&g->sh_unsup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const uint32_t E = w.E;
+  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
+  uint32_t cls = 0, code = TB_CT_OK;
+  if (i < E) {
+    cls = s.cls[i];
+    code = s.code[i];
+  }
+  bool ins = (cls & C_INSERTED) != 0;
+  const uint32_t bad = code != TB_CT_OK;
+  const uint32_t pbad = seg_prefix<SEG>(s.cnt_bad, blockIdx.x, lds);
+  const uint32_t pins = seg_prefix<SEG>(s.cnt_ins, blockIdx.x, lds);
+  uint32_t tot_bad, tot_ins;
+  const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
+  const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
+  if (i >= E) return;
+  if (unsup) {
+    if (i == 0) atomicOr(&g->window_error, 2u);
+    if (i == E - 1) sh_window_reset(g, XFER, 0, false);
+    return;
+  }
+  const uint64_t xbase = XFER ? g->x_count : g->acc_count;
+  const uint32_t b = s.batch[i];
+  if (i == w.off[b]) {
+    for (int32_t bb = (int32_t)b; bb >= 0 && w.off[bb] == i; bb--) o.batch_base[bb] = rbad;
+  }
+  if (bad && sh_guard(g, rbad < E, 2, rbad)) {
+    tb_create_result_t r;
+    r.index = i - w.off[b];
+    r.result = code;
+    o.results[rbad] = r;
+  }
+  if (XFER) {
+    uint32_t drs = s.dr_slot[i], crs = s.cr_slot[i];
+    if (drs != NONE32 && !sh_guard(g, drs < d.acc_max, 3, drs)) drs = NONE32;
+    if (crs != NONE32 && !sh_guard(g, crs < d.acc_max, 4, crs)) crs = NONE32;
+    if (ins && !sh_guard(g, xbase + rins < d.x_max, 5, xbase + rins)) ins = false;
+    if ((cls & C_COMMIT) && ((drs != NONE32) | (crs != NONE32) | ins)) {
+      tb_transfer_t t2 = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
+      const u128 a = U(t2.amount);
+      Add128 adds[2];
+      int nadd = 0;
+      if (drs != NONE32) adds[nadd++].issue(&d.acc[drs].debits_posted, a);
+      if (crs != NONE32) adds[nadd++].issue(&d.acc[crs].credits_posted, a);
+      if (ins) {
+        const uint64_t slot = xbase + rins;
+        t2.timestamp = win_ts(w, b, i);
+        d.xr[slot] = t2;
+        x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
+        d.xstatus[slot] = 0;
+      }
+      for (int k = 0; k < nadd; k++) adds[k].finish();
+    }
+  } else if (ins && sh_guard(g, xbase + rins < d.acc_max, 6, xbase + rins)) {
+    const uint64_t slot = xbase + rins;
+    tb_account_t a = reinterpret_cast<const tb_account_t*>(ev_bytes)[i];
+    a.timestamp = win_ts(w, b, i);
+    d.acc[slot] = a;
+    d.hot[slot] = 0;
+    acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
+  }
+  if (i == E - 1) {
+    const uint32_t total_bad = rbad + bad, total_ins = rins + (ins ? 1u : 0u);
+    for (int32_t bb = (int32_t)w.nb; bb >= 0 && w.off[bb] == E; bb--) o.batch_base[bb] = total_bad;
+    if (o.out_count) *o.out_count = total_bad;
+    g->result_count = total_bad;
+    g->events_total += E;
+    sh_window_reset(g, XFER, xbase + total_ins, true);
+  }
+}

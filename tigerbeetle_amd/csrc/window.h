@@ -52,6 +52,7 @@ struct Dev {
   ExpEntry* exp[2];
   uint32_t* exp_cur;  // device word selecting the live expiry buffer
   Globals* g;
+  uint64_t acc_max, x_max;  // store capacities (records)
 };
 
 struct Scratch {

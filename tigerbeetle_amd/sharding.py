@@ -1,0 +1,110 @@
+"""Hash-sharded commit over the GPUs of one node: one engine per GPU, one process per GPU.
+
+Account a lives on shard `shard_of(a.id)`, transfer t on shard `shard_of(t.id)` (csrc/shard.h).
+Every shard receives the same prepared window (the replica hands each GPU the same prepare body,
+state_machine.zig:1107-1146) and commits it in three steps through the C ABI (include/tbg.h):
+
+  tbg_shard_prepare_window   validate; resolve the owned accounts / ids; write exchange words
+  exchange                   element-wise int32 sum of the exchange words across the shards, on the
+                             engine's stream (RCCL all-reduce over xGMI: torch.distributed "nccl")
+  tbg_shard_commit_window    decide every event (identically on every shard); owned effects only
+
+The `exchange` callable is the only collective on the data path; with one shard there is none.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .state_machine import StateMachine
+
+_M1, _M2 = np.uint64(0xFF51AFD7ED558CCD), np.uint64(0xC4CEB9FE1A85EC53)
+
+
+def _mix64(x):
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint64(33))
+        x = x * _M1
+        x = x ^ (x >> np.uint64(33))
+        x = x * _M2
+        return x ^ (x >> np.uint64(33))
+
+
+def shard_of(id_lo, id_hi, shard_count):
+    """Numpy twin of shard_of() in csrc/shard.h (high half of the table hash, scaled to G)."""
+    lo = np.asarray(id_lo, np.uint64)
+    hi = np.asarray(id_hi, np.uint64)
+    with np.errstate(over="ignore"):
+        h = _mix64(lo ^ _mix64(hi + np.uint64(0x9E3779B97F4A7C15)))
+        return (((h >> np.uint64(32)) * np.uint64(shard_count)) >> np.uint64(32)).astype(np.uint32)
+
+
+def exchange_nccl(t):
+    """In-place sum across the process group on the current (engine) stream: RCCL on ROCm."""
+    import torch.distributed as dist
+
+    dist.all_reduce(t)
+
+
+def exchange_gloo(t):
+    """Same reduction through host memory (gloo): for ranks that share one GPU in tests."""
+    import torch.distributed as dist
+
+    c = t.cpu()
+    dist.all_reduce(c)
+    t.copy_(c)
+
+
+class ShardedStateMachine:
+    """One shard of a hash-sharded engine. `exchange(t)` must sum the int32 tensor `t` in place
+    across all shards (None for a single shard)."""
+
+    def __init__(self, shard_count, shard_index, exchange=None, device=0, batch_max=8190, accounts_max=1 << 16,
+                 transfers_max=1 << 20, window_events_max=0):
+        import torch
+
+        self.sm = StateMachine(device=device, batch_max=batch_max, accounts_max=accounts_max,
+                               transfers_max=transfers_max, window_events_max=window_events_max,
+                               shard_count=shard_count, shard_index=shard_index)
+        self.shard_count, self.shard_index = shard_count, shard_index
+        self.exchange = exchange
+        events_max = window_events_max or batch_max
+        self.xch = torch.zeros((events_max + 1) * 4, dtype=torch.int32, device=torch.device("cuda", device))
+        self.stream = torch.cuda.ExternalStream(self.sm.stream, device=torch.device("cuda", device))
+        torch.cuda.synchronize(device)
+
+    @property
+    def h(self):
+        return self.sm.h
+
+    def close(self):
+        self.sm.close()
+
+    def prepare_window(self, operation, d_events, batch_events, batch_timestamps):
+        nb = len(batch_events)
+        ev = (ctypes.c_uint32 * nb)(*batch_events)
+        ts = (ctypes.c_uint64 * nb)(*batch_timestamps)
+        _lib.check(_lib.lib().tbg_shard_prepare_window(self.sm.h, int(operation), d_events, nb, ev, ts,
+                                                       self.xch.data_ptr()), "shard_prepare_window")
+        return self.xch[: 4 * (sum(batch_events) + 1)]
+
+    def commit_prepared(self, d_results, d_batch_base):
+        _lib.check(_lib.lib().tbg_shard_commit_window(self.sm.h, self.xch.data_ptr(), d_results, d_batch_base),
+                   "shard_commit_window")
+
+    def commit_window(self, operation, d_events, batch_events, batch_timestamps, d_results, d_batch_base):
+        """Asynchronous on the engine stream; results land in d_results / d_batch_base exactly as
+        tbg_commit_window's (identical on every shard)."""
+        import torch
+
+        words = self.prepare_window(operation, d_events, batch_events, batch_timestamps)
+        if self.exchange is not None:
+            with torch.cuda.stream(self.stream):
+                self.exchange(words)
+        self.commit_prepared(d_results, d_batch_base)
+
+    def sync(self):
+        self.sm.sync()
+
+    def stats(self):
+        return self.sm.stats()

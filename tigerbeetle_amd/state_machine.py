@@ -17,10 +17,11 @@ MESSAGE_BODY_SIZE_MAX = 1048576 - 256
 
 class StateMachine:
     def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20,
-                 window_events_max=0, resolver=True, components=True):
+                 window_events_max=0, resolver=True, components=True, shard_count=0, shard_index=0):
         L = _lib.lib()
         flags = (0 if resolver else _lib.FLAG_NO_RESOLVER) | (0 if components else _lib.FLAG_NO_COMPONENTS)
-        cfg = _lib.Config(device, batch_max, accounts_max, transfers_max, window_events_max, flags)
+        cfg = _lib.Config(device, batch_max, accounts_max, transfers_max, window_events_max, flags, shard_count,
+                          shard_index)
         h = ctypes.c_void_p()
         _lib.check(L.tbg_create(ctypes.byref(cfg), ctypes.byref(h)), "tbg_create")
         self.h = h
