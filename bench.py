@@ -8,6 +8,10 @@ src/tigerbeetle/benchmark_load.zig:206-327). `--config` selects the other BASELI
         pre-funded from treasury accounts (funding untimed), 10M transfers
   cfg4  two-phase (30 % pending, post/void, expiry) + linked chains with injected failures,
         synthetic clock +1 s per batch (a pulse is due before every batch), 10M transfers
+  cfg5  hash-sharded over the N GPUs (default when N > 1): 12.5M accounts and 125M uniform transfers
+        per GPU (100M / 1B at N = 8), ~(N-1)/N of the transfers cross-shard; one stream for the whole
+        job, resident in every GPU's HBM; per window one RCCL all-reduce of the per-event owner facts
+        (tigerbeetle_amd/sharding.py, csrc/shard.h)
 
 A "step" is one create_transfers batch of the stream, committed through the engine's
 device-resident C ABI in windows of --window consecutive batches (tbg_commit_window: pulse
@@ -16,8 +20,10 @@ state_machine.zig:2719-2739). The first W batches are warmup; the next K are tim
 barrier + stream syncs, max over ranks. `value` counts every committed event (failed ones too:
 they are committed with a result code); `results.ok_events_per_s` counts the successful ones.
 
-Multi-GPU (torchrun, one rank per GPU): every rank owns an independent account shard and its own
-stream of the same shape (weak scaling, no data-path collective).
+Multi-GPU (torchrun, one rank per GPU): cfg5 shards one global stream over the ranks (accounts and
+transfer ids hash-partitioned, cross-shard facts exchanged by RCCL all-reduce; weak scaling: the
+stream grows with N). cfg1-cfg4 at N > 1 run one independent account shard per rank with its own
+stream (no data-path collective). See DESIGN.md §7.
 
 Extra JSON fields: `roofline` for the dominant kernel (HIP events on the engine stream over the
 timed region) and `cpu_baseline` (the single-threaded C restatement, oracle/, on a bounded prefix
@@ -55,6 +61,8 @@ CONFIGS = {
     "cfg2": dict(accounts=1_000_000, transfers=100_000_000, window=32, seed=44, tick=0),
     "cfg3": dict(accounts=1_000_000, transfers=10_000_000, window=32, seed=45, tick=0),
     "cfg4": dict(accounts=1_000_000, transfers=10_000_000, window=1, seed=46, tick=NS_PER_S),
+    # per GPU (weak scaling): 100M accounts / 1B transfers at 8 GPUs
+    "cfg5": dict(accounts=12_500_000, transfers=125_000_000, window=64, seed=47, tick=0),
 }
 CFG3_TREASURY, CFG3_TOP, CFG3_FUND, CFG3_FUND_ID = 1000, 1000, 1_000_000, 10**15
 
@@ -62,7 +70,10 @@ CFG3_TREASURY, CFG3_TOP, CFG3_FUND, CFG3_FUND_ID = 1000, 1000, 1_000_000, 10**15
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    p.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                   help="default: cfg2 on one GPU, cfg5 (sharded) on several")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process group; gloo lets ranks share one GPU (rehearsal), exchange via host")
     p.add_argument("--steps", type=int, default=None, help="timed batches (default: rest of the stream)")
     p.add_argument("--warmup", type=int, default=None, help="warmup batches (rounded to whole windows)")
     p.add_argument("--window", type=int, default=None, help="batches per commit window (super-batching)")
@@ -74,6 +85,8 @@ def parse():
     p.add_argument("--no-phase-timing", action="store_true")
     p.add_argument("--verify", action="store_true", help="setup all ok; cfg1/cfg2: every transfer ok")
     a = p.parse_args()
+    if a.config is None:
+        a.config = "cfg5" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "cfg2"
     c = CONFIGS[a.config]
     for k in ("accounts", "transfers", "window", "seed"):
         if getattr(a, k) is None:
@@ -163,6 +176,173 @@ def cpu_baseline(args, seed):
     }
 
 
+# Algorithmic bytes per event of the sharded kernels on one of G shards: every shard
+# reads each event and writes its exchange word and scratch; owned probes / effects are 1/G each.
+def shard_kernel_bytes(kernel, G):
+    if kernel == "prep":
+        # event 128, exchange word 16, scratch 22; owned: 2 account-table entries, id-table entry,
+        # key-map entry
+        return 128 + 16 + 22 + (2 * 32 + 32 + 16) / G
+    # final: scratch 8, replies; owned: event re-read 128, record append 128, id-table entry 32,
+    # two balance pairs read+write 2 x 64
+    return 8 + (128 + 128 + 32 + 2 * 64) / G
+
+
+def run_sharded(args, torch, dist, world, rank, device):
+    """cfg5: one global stream, hash-sharded over the ranks (tigerbeetle_amd/sharding.py)."""
+    from tigerbeetle_amd import _lib
+    from tigerbeetle_amd.sharding import ShardedStateMachine, exchange_gloo, exchange_nccl
+    from tigerbeetle_amd.state_machine import to_host
+    from tigerbeetle_amd.types import Operation
+
+    L = _lib.lib()
+    G, me = world, rank
+    n_acc = args.accounts * G
+    total_batches = (args.transfers * G + BATCH - 1) // BATCH
+    win = max(1, min(args.window, 64))
+    warm = min(((args.warmup + win - 1) // win) * win, max(0, total_batches - win))
+    steps = args.steps if args.steps is not None else total_batches - warm
+    n_batches = min(total_batches, warm + steps)
+    n_xfer = min(args.transfers * G, n_batches * BATCH)
+    exchange = None if G == 1 else (exchange_gloo if args.backend == "gloo" else exchange_nccl)
+    acc_cap = n_acc if G == 1 else int(n_acc / G * 1.02) + 65536
+    x_cap = n_xfer if G == 1 else int(n_xfer / G * 1.02) + win * BATCH
+    sm = ShardedStateMachine(G, me, exchange, device=device, batch_max=BATCH, accounts_max=acc_cap,
+                             transfers_max=x_cap, window_events_max=win * BATCH)
+    stream = sm.sm.stream
+
+    # The whole job's stream, identical and resident on every GPU before timing.
+    d_acc = torch.empty(n_acc * 128, dtype=torch.uint8, device="cuda")
+    d_xfer = torch.empty(n_xfer * 128, dtype=torch.uint8, device="cuda")
+    d_res = torch.empty(win * BATCH * 8, dtype=torch.uint8, device="cuda")
+    n_windows_max = (max(n_batches, (n_acc + BATCH - 1) // BATCH) + win - 1) // win + 1
+    d_base = torch.zeros(n_windows_max * 65, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    _lib.check(L.tbg_gen_accounts(d_acc.data_ptr(), 0, n_acc, args.seed, 2, 1, 0, stream), "gen accounts")
+    _lib.check(L.tbg_gen_transfers_uniform(d_xfer.data_ptr(), 0, n_xfer, args.seed, n_acc, 0, stream), "gen")
+    sm.stream.synchronize()
+
+    prepare_ts = 0
+
+    def commit_range(op, d_events, first_batch, last_batch, n_total, widx):
+        nonlocal prepare_ts
+        ns, ts = [], []
+        for b in range(first_batch, last_batch):
+            n = min(BATCH, n_total - b * BATCH)
+            prepare_ts += 1 + n
+            ns.append(n)
+            ts.append(prepare_ts)
+        sm.commit_window(op, d_events.data_ptr() + first_batch * BATCH * 128, ns, ts, d_res.data_ptr(),
+                         d_base.data_ptr() + widx * 65 * 4)
+        return widx, len(ns)
+
+    def failures(wins):
+        bases = to_host(d_base).reshape(-1, 65)
+        return int(sum(bases[wi, nb] for wi, nb in wins))
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    nb_acc = (n_acc + BATCH - 1) // BATCH
+    wins = [commit_range(Operation.create_accounts, d_acc, b0, min(b0 + win, nb_acc), n_acc, i)
+            for i, b0 in enumerate(range(0, nb_acc, win))]
+    sm.sync()
+    acc_fail = failures(wins)
+    d_base.zero_()
+
+    widx = 0
+    warm_windows = []
+    for b0 in range(0, warm, win):
+        warm_windows.append(commit_range(Operation.create_transfers, d_xfer, b0, min(b0 + win, warm), n_xfer, widx))
+        widx += 1
+    sm.sync()
+    NPH = len(PHASES)
+    L.tbg_timing_collect(sm.h, (ctypes.c_double * NPH)(), (ctypes.c_uint64 * NPH)(), NPH)  # reset
+    L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else 1)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    timed_windows = []
+    for b0 in range(warm, n_batches, win):
+        timed_windows.append(commit_range(Operation.create_transfers, d_xfer, b0, min(b0 + win, n_batches), n_xfer,
+                                          widx))
+        widx += 1
+    sm.sync()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    barrier()
+    L.tbg_timing_enable(sm.h, 0)
+    ms = (ctypes.c_double * NPH)()
+    launches = (ctypes.c_uint64 * NPH)()
+    L.tbg_timing_collect(sm.h, ms, launches, NPH)
+
+    timed_batches = n_batches - warm
+    timed_events = n_xfer - warm * BATCH  # global: every shard commits the same stream once
+    timed_fails = failures(timed_windows)
+    fails = failures(warm_windows) + timed_fails
+    elapsed = wall
+    if dist:
+        dev = "cpu" if args.backend == "gloo" else "cuda"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = sm.stats()
+    if args.verify:
+        assert acc_fail == 0 and fails == 0, (acc_fail, fails)
+    if rank == 0:
+        per_phase = {PHASES[p]: (ms[p] / launches[p] * 1000.0 if launches[p] else None) for p in range(NPH)}
+        dom = max(("prep", "final"), key=lambda k: per_phase[k] or 0.0)
+        roof = None
+        if per_phase[dom]:
+            us = per_phase[dom]
+            ev_per_launch = timed_events / max(launches[PHASES.index(dom)], 1)
+            bytes_launch = int(shard_kernel_bytes(dom, G) * ev_per_launch)
+            achieved = bytes_launch / (us * 1e-6) / 1e9
+            kname = {"prep": "k_sh_prep_ct", "final": "k_sh_final<true>"}[dom]
+            roof = {"bound": "hbm", "kernel": kname, "events_per_launch": int(ev_per_launch),
+                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
+                    "phase_avg_us": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
+                    "exchange_bytes_per_window_per_gpu": 16 * (win * BATCH + 1)}
+        line = {
+            "metric": "committed transfers/sec (create_transfers)",
+            "value": round(timed_events / elapsed, 1),
+            "unit": "transfers/s",
+            "n_gpus": world,
+            "steps": timed_batches,
+            "warmup": warm,
+            "ms_per_step": round(elapsed * 1000.0 / timed_batches, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u128",
+            "data": "synthetic (device-generated, seed %d, same stream on every GPU)" % args.seed,
+            "config": {"workload": "cfg5: %d accounts hash-sharded over %d GPU(s), %d uniform create_transfers "
+                                   "(%.1f %% cross-shard), %d/batch" % (n_acc, G, n_xfer, 100.0 * (G - 1) / G, BATCH),
+                       "batch": BATCH, "window_batches": win, "accounts_per_gpu": args.accounts,
+                       "transfers_per_gpu": args.transfers,
+                       "parallelism": "hash-sharded accounts+ids, RCCL all-reduce per window" if G > 1 else
+                                      "single shard"},
+            "results": {"failed_events_timed": int(timed_fails),
+                        "ok_events_per_s": round((timed_events - timed_fails) / elapsed, 1),
+                        "shard0_accounts": st["accounts"], "shard0_transfers": st["transfers"],
+                        "backend": args.backend if G > 1 else None, "wall_ms_timed": round(wall * 1000, 3)},
+            "roofline": roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            import copy
+
+            a2 = copy.copy(args)
+            a2.accounts, a2.transfers = n_acc, n_xfer
+            line["cpu_baseline"] = cpu_baseline(a2, args.seed)
+        print(json.dumps(line), flush=True)
+    sm.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     import torch
@@ -175,13 +355,20 @@ def main():
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "gloo":  # rehearsal: ranks may share a GPU
+            torch.cuda.set_device(local_rank % torch.cuda.device_count())
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
     device = torch.cuda.current_device()
+    if args.config == "cfg5":
+        return run_sharded(args, torch, dist, world, rank, device)
 
     from tigerbeetle_amd import StateMachine, _lib, workload
+    from tigerbeetle_amd.state_machine import to_host
     from tigerbeetle_amd.types import Operation
 
     L = _lib.lib()
@@ -242,7 +429,7 @@ def main():
         return widx, len(ns)
 
     def failures(wins):
-        bases = d_base.view(-1, 65).cpu().numpy()
+        bases = to_host(d_base).reshape(-1, 65)
         return int(sum(bases[wi, nb] for wi, nb in wins))
 
     def commit_all(op, d_events, n_total):

@@ -8,6 +8,7 @@ from oracle_sm import OracleStateMachine
 from test_gpu_parity import _compare_final
 from test_gpu_window import commit_window, oracle_batches
 from tigerbeetle_amd import workload
+from tigerbeetle_amd.state_machine import to_host
 from tigerbeetle_amd.types import ACCOUNT_DTYPE, NS_PER_S, TRANSFER_DTYPE, Operation
 
 BM = 8190
@@ -22,7 +23,7 @@ def _device_gen(fn, count, dtype, *args):
     torch.cuda.synchronize()
     _lib.check(fn(d.data_ptr(), *args, None), "gen")
     torch.cuda.synchronize()
-    return np.frombuffer(d.cpu().numpy().tobytes(), dtype)
+    return np.frombuffer(to_host(d).tobytes(), dtype)
 
 
 @pytest.mark.gpu

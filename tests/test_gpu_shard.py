@@ -10,6 +10,7 @@ import pytest
 from oracle_sm import OracleStateMachine
 from test_gpu_window import oracle_batches
 from tigerbeetle_amd import workload
+from tigerbeetle_amd.state_machine import to_host
 from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE, Operation
 
 BM = 8190
@@ -62,8 +63,8 @@ class LocalShards:
             s.sync()
         replies = []
         for d_res, d_base in outs:
-            res = d_res.cpu().numpy().tobytes()
-            base = d_base.cpu().numpy()
+            res = to_host(d_res).tobytes()
+            base = to_host(d_base)
             replies.append([res[base[b] * 8: base[b + 1] * 8] for b in range(len(ns))])
         assert all(r == replies[0] for r in replies[1:]), "shards disagree on the replies"
         return replies[0]

@@ -8,6 +8,7 @@ from chaos import Chaos, run_protocol
 from oracle_sm import OracleStateMachine
 from test_gpu_parity import _compare_final
 from tigerbeetle_amd import workload
+from tigerbeetle_amd.state_machine import to_host
 from tigerbeetle_amd.types import NS_PER_S, RESULT_DTYPE, Operation
 
 
@@ -28,8 +29,8 @@ def commit_window(sm, op, batches, tick_ns=0):
     torch.cuda.synchronize()
     sm.commit_window(op, d_ev.data_ptr(), ns, ts, d_res.data_ptr(), d_base.data_ptr(), True, ts[0])
     sm.sync()
-    res = d_res.cpu().numpy().tobytes()
-    base = d_base.cpu().numpy()
+    res = to_host(d_res).tobytes()
+    base = to_host(d_base)
     return [res[base[b] * 8: base[b + 1] * 8] for b in range(len(ns))]
 
 

@@ -1,0 +1,131 @@
+"""CPU tests of the hash-sharded path (no GPU): the ownership hash matches the library's, and the
+sharded decomposition (owner facts -> all-reduce -> identical decide -> owned effects) reproduces the
+CPU restatement, with real gloo collectives at world size 2 and 3."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from tigerbeetle_amd.sharding import shard_of
+
+BM = 64
+
+
+def test_shard_of_matches_library():
+    from tigerbeetle_amd import _lib
+
+    L = _lib.lib()
+    rng = np.random.default_rng(0)
+    lo = rng.integers(0, 2**63, 2000, dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+    hi = np.where(rng.integers(0, 4, 2000) == 0, rng.integers(0, 2**63, 2000, dtype=np.uint64), 0).astype(np.uint64)
+    for G in (1, 2, 3, 7, 8):
+        got = shard_of(lo, hi, G)
+        want = [L.tbg_shard_of(int(a), int(b), G) for a, b in zip(lo, hi)]
+        assert got.tolist() == want
+        assert set(got.tolist()) == set(range(G))  # every shard owns something
+
+
+def test_shard_of_balances_sequential_ids():
+    ids = np.arange(1, 800_001, dtype=np.uint64)
+    counts = np.bincount(shard_of(ids, np.zeros_like(ids), 8), minlength=8)
+    assert counts.min() > 0.98 * len(ids) / 8
+
+
+def _stream(seed, n_acc, n_batches):
+    """Mixed create_accounts / create_transfers batches inside the sharded class."""
+    from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE
+
+    rng = np.random.default_rng(seed)
+    out = []
+    a = np.zeros(n_acc, ACCOUNT_DTYPE)
+    a["id_lo"] = rng.permutation(np.arange(1, n_acc + 1, dtype=np.uint64))
+    a["ledger"] = 1 + a["id_lo"] % 2
+    a["code"] = 1
+    a["flags"] = np.where(rng.integers(0, 10, n_acc) == 0, 1, 0)
+    a["reserved"] = np.where(rng.integers(0, 40, n_acc) == 0, 1, 0)
+    out += [("a", a[i:i + BM]) for i in range(0, n_acc, BM)]
+    again = a[: BM].copy()
+    again["user_data_64"] = rng.integers(0, 2, BM)
+    out.append(("a", again))
+    next_id = 1
+    for _ in range(n_batches):
+        n = int(rng.integers(1, BM + 1))
+        t = np.zeros(n, TRANSFER_DTYPE)
+        t["id_lo"] = np.arange(next_id, next_id + n, dtype=np.uint64)
+        if next_id > 200:
+            k = min(n // 6, 10)
+            t["id_lo"][:k] = rng.choice(np.arange(1, next_id - 1, dtype=np.uint64), k, replace=False)
+        next_id += n
+        dr = rng.integers(1, n_acc + 5, n)
+        cr = rng.integers(1, n_acc + 5, n)
+        t["debit_account_id_lo"] = dr
+        t["credit_account_id_lo"] = cr
+        t["amount_lo"] = rng.integers(0, 500, n)
+        t["ledger"] = np.where(rng.integers(0, 20, n) == 0, 2 - dr % 2, 1 + dr % 2)
+        t["code"] = rng.integers(0, 4, n)
+        t["user_data_32"] = rng.integers(0, 2, n)
+        t["flags"] = np.where(rng.integers(0, 7, n) == 0, 1, 0)
+        t["timestamp"] = np.where(rng.integers(0, 80, n) == 0, 3, 0)
+        out.append(("t", t))
+    return out
+
+
+def _rank(rank, world, port, seed, n_acc, n_batches, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    from shard_model import ShardModel
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = ShardModel(world, rank)
+    T, replies = 0, []
+    for op, ev in _stream(seed, n_acc, n_batches):
+        T += 1 + len(ev)
+        words, static = m.prep(op, ev)
+        w = torch.from_numpy(words)
+        dist.all_reduce(w)  # the only collective: owner facts summed across shards
+        codes = m.decide(op, ev, w.numpy(), static)
+        m.apply(op, ev, codes, T, len(ev))
+        replies.append(np.array([(i, c) for i, c in enumerate(codes) if c != 0], np.uint32).reshape(-1, 2))
+    np.save(os.path.join(out_dir, f"acc{rank}.npy"), np.array(list(m.accounts.values())))
+    np.save(os.path.join(out_dir, f"xfer{rank}.npy"), np.array(list(m.transfers.values())))
+    np.save(os.path.join(out_dir, f"rep{rank}.npy"), np.concatenate(
+        [np.concatenate([[[len(r), 0]], r]).astype(np.uint32) for r in replies]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_protocol_matches_oracle(world, tmp_path):
+    import torch.multiprocessing as mp
+
+    from chaos import run_protocol
+    from oracle_sm import OracleStateMachine
+    from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE, Operation
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    seed, n_acc, n_batches = 11, 150, 40
+    mp.spawn(_rank, args=(world, port, seed, n_acc, n_batches, str(tmp_path)), nprocs=world, join=True)
+    ref = OracleStateMachine(batch_max=BM)
+    try:
+        parts = []
+        for op, ev in _stream(seed, n_acc, n_batches):
+            r = run_protocol(ref, Operation.create_accounts if op == "a" else Operation.create_transfers, ev)
+            rr = np.frombuffer(r, np.uint32).reshape(-1, 2)
+            parts.append(np.concatenate([[[len(rr), 0]], rr]).astype(np.uint32))
+        expect = np.concatenate(parts)
+        assert (expect[:, 1] != 0).any()
+        for r in range(world):
+            assert np.array_equal(np.load(tmp_path / f"rep{r}.npy"), expect), f"rank {r}"
+        acc = np.concatenate([np.load(tmp_path / f"acc{r}.npy").astype(ACCOUNT_DTYPE) for r in range(world)])
+        xfer = np.concatenate([np.load(tmp_path / f"xfer{r}.npy").astype(TRANSFER_DTYPE) for r in range(world)])
+        acc = acc[np.argsort(acc["timestamp"], kind="stable")]
+        xfer = xfer[np.argsort(xfer["timestamp"], kind="stable")]
+        assert acc.tobytes() == ref.dump_accounts().tobytes()
+        assert xfer.tobytes() == ref.dump_transfers().tobytes()
+    finally:
+        ref.close()

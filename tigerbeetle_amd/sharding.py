@@ -47,12 +47,17 @@ def exchange_nccl(t):
 
 
 def exchange_gloo(t):
-    """Same reduction through host memory (gloo): for ranks that share one GPU in tests."""
+    """Same reduction through host memory (gloo): for ranks that share one GPU in tests. Copies go
+    through pinned memory on the current (engine) stream and are waited for explicitly."""
+    import torch
     import torch.distributed as dist
 
-    c = t.cpu()
+    c = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    c.copy_(t, non_blocking=True)
+    torch.cuda.current_stream().synchronize()
     dist.all_reduce(c)
-    t.copy_(c)
+    t.copy_(c, non_blocking=True)
+    torch.cuda.current_stream().synchronize()
 
 
 class ShardedStateMachine:

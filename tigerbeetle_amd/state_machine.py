@@ -15,6 +15,18 @@ from .types import ACCOUNT_DTYPE, BATCH_MAX, TRANSFER_DTYPE, Operation
 MESSAGE_BODY_SIZE_MAX = 1048576 - 256
 
 
+def to_host(t):
+    """Device tensor -> numpy copy through pinned memory, waited for on the current stream.
+    (Pageable device->host copies were observed returning before every byte landed on this stack
+    while other streams were active)"""
+    import torch
+
+    c = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    c.copy_(t, non_blocking=True)
+    torch.cuda.current_stream().synchronize()
+    return c.numpy().copy()
+
+
 class StateMachine:
     def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20,
                  window_events_max=0, resolver=True, components=True, shard_count=0, shard_index=0):
@@ -32,9 +44,9 @@ class StateMachine:
         self._out = np.zeros(MESSAGE_BODY_SIZE_MAX, np.uint8)
 
     def close(self):
-        if getattr(self, "h", None):
-            _lib.lib().tbg_destroy(self.h)
-            self.h = None
+        h, self.h = getattr(self, "h", None), None
+        if h and _lib is not None and _lib.lib is not None:  # module globals may be gone at exit
+            _lib.lib().tbg_destroy(h)
 
     def __del__(self):
         self.close()
