@@ -67,6 +67,24 @@ CONFIGS = {
 CFG3_TREASURY, CFG3_TOP, CFG3_FUND, CFG3_FUND_ID = 1000, 1000, 1_000_000, 10**15
 
 
+def pmc_traffic(config, kernel, events_per_launch):
+    """Per-launch HBM traffic of `kernel` from the committed rocprofv3 PMC summary of this config
+    (profiles/r1/pmc_<config>.json, made by tools/profile.sh + tools/pmc_summary.py: separate
+    FETCH_SIZE and WRITE_SIZE passes over the same bench command), scaled to this run's events per
+    launch. Returns (raw FETCH+WRITE bytes, bytes with FETCH doubled per the gfx950 streaming-read
+    correction, source) or None."""
+    path = os.path.join(ROOT, "profiles", "r1", "pmc_%s.json" % config)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        k = json.load(f)["kernels"].get(kernel)
+    if not k:
+        return None
+    scale = events_per_launch / max(k["grid"], 1)
+    return (round(k["traffic_bytes"] * scale), round(k["traffic_fetch_x2_bytes"] * scale),
+            os.path.relpath(path, ROOT))
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -300,9 +318,11 @@ def run_sharded(args, torch, dist, world, rank, device):
             bytes_launch = int(shard_kernel_bytes(dom, G) * ev_per_launch)
             achieved = bytes_launch / (us * 1e-6) / 1e9
             kname = {"prep": "k_sh_prep_ct", "final": "k_sh_final<true>"}[dom]
+            tr = pmc_traffic("cfg5", kname, ev_per_launch) if G == 1 else None
             roof = {"bound": "hbm", "kernel": kname, "events_per_launch": int(ev_per_launch),
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
+                    "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
                     "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
                     "phase_avg_us": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
                     "exchange_bytes_per_window_per_gpu": 16 * (win * BATCH + 1)}
@@ -515,9 +535,11 @@ def main():
             bytes_launch = int(KERNEL_BYTES_PER_EVENT[dom] * ev_per_launch)
             achieved = bytes_launch / (us * 1e-6) / 1e9
             kname = {"prep": "k_ct_prep", "final": "k_final<true>"}[dom]
+            tr = pmc_traffic(cfg, kname, ev_per_launch)
             roof = {"bound": "hbm", "kernel": kname, "events_per_launch": int(ev_per_launch),
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
+                    "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
                     "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
                     "phase_avg_us": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
                     "path_alg_GBs": round(640 * all_events / elapsed / 1e9 / max(world, 1), 1)}
