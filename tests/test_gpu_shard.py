@@ -59,8 +59,13 @@ class LocalShards:
             torch.cuda.synchronize()
             s.commit_prepared(d_res.data_ptr(), d_base.data_ptr())
             outs.append((d_res, d_base))
-        for s in self.shards:
-            s.sync()
+        for r, s in enumerate(self.shards):
+            try:
+                s.sync()
+            except RuntimeError as e:
+                if "status -3" in str(e):
+                    raise RuntimeError(f"shard {r}: {e}; {self._diagnose(r, op, batches)}") from e
+                raise
         replies = []
         for d_res, d_base in outs:
             res = to_host(d_res).tobytes()
@@ -68,6 +73,26 @@ class LocalShards:
             replies.append([res[base[b] * 8: base[b + 1] * 8] for b in range(len(ns))])
         assert all(r == replies[0] for r in replies[1:]), "shards disagree on the replies"
         return replies[0]
+
+    def _diagnose(self, r, op, batches):
+        """Invariants of the failed window's per-event class bits (C_OWN 1<<18, C_INSERTED 1<<14,
+        C_COMMIT 1<<13) and codes, read back from shard r."""
+        from tigerbeetle_amd import _lib
+        from tigerbeetle_amd.sharding import shard_of
+
+        ev = np.concatenate(batches)
+        n = len(ev)
+        cls = np.zeros(n, np.uint32)
+        code = np.zeros(n, np.uint32)
+        _lib.lib().tbg_debug_last_batch(self.shards[r].h, cls.ctypes.data, code.ctypes.data, n)
+        G = len(self.shards)
+        own = shard_of(ev["id_lo"], ev["id_hi"], G) == r
+        c_own, c_ins = (cls >> 18) & 1 == 1, (cls >> 14) & 1 == 1
+        ok = code == 0
+        return (f"events {n}, C_OWN {int(c_own.sum())} (hash-owned {int(own.sum())}, mismatched "
+                f"{int((c_own != own).sum())}), C_INSERTED {int(c_ins.sum())} (owned ok {int((own & ok).sum())}, "
+                f"inserted-not-owned {int((c_ins & ~c_own).sum())}), codes not ok {int((~ok).sum())}, "
+                f"stats {self.shards[r].stats()}")
 
     def dump_accounts(self):
         a = np.concatenate([s.sm.dump_accounts() for s in self.shards])

@@ -5,7 +5,9 @@
 //                                flags): the transfer path resolves an account and checks ledger and
 //                                limit flags from this one line, never touching the 128 B record.
 //   acc      tb_account_t[]      dense Account records in creation (= timestamp) order.
-//   x_tab    XEntry[x_cap]       id -> slot table for transfers, 32 B entries.
+//   x_tab    XEntry[x_cap]       id -> slot table for transfers, 8 B entries {fingerprint, slot}: one
+//                                64-bit CAS inserts; a fingerprint hit is confirmed against the
+//                                stored record's id (the caller reads that record anyway).
 //   xr       tb_transfer_t[]     dense Transfer records in commit (= timestamp) order.
 //   xstatus  u8[]                TransferPending.status per transfer slot (0 = none). Keyed by slot
 //                                instead of by timestamp: slot order == timestamp order, 1:1.
@@ -34,13 +36,8 @@ struct __attribute__((aligned(32))) AccEntry {
 };
 static_assert(sizeof(AccEntry) == 32, "AccEntry");
 
-struct __attribute__((aligned(32))) XEntry {
-  uint64_t id_lo, id_hi;
-  uint32_t slot;  // NONE32 = empty
-  uint32_t pad0;
-  uint64_t pad1;
-};
-static_assert(sizeof(XEntry) == 32, "XEntry");
+typedef unsigned long long XEntry;  // [63:32] high half of the id hash, [31:0] record slot
+#define X_EMPTY 0xFFFFFFFFFFFFFFFFull  // slot NONE32 never occurs in a live entry
 
 // Window-local key map. Entries are epoch-tagged (the window number), so a stale entry from an
 // earlier window reads as empty and nothing is ever reset. Keys are never stored: `key` names the
@@ -106,6 +103,8 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t cc_count;    // components of W
   uint32_t cpw_done;    // the component walkers decided every W event
   uint64_t cpw_events_total;  // cumulative W events decided by component walkers
+  uint64_t x_id_max;    // >= every stored transfer id (u64 max once any id needs > 64 bits): an id
+                        // above it cannot exist, so its table probe is skipped (monotonic ids)
   // sharded engines (shard.h), per window
   uint32_t sh_blocks;   // prep blocks finished (the last one closes the trailer word)
   uint32_t sh_unsup;    // the window is outside the sharded class: nothing is applied
@@ -186,16 +185,32 @@ __device__ inline uint32_t acc_find(const AccEntry* __restrict__ tab, uint64_t m
   }
 }
 
-__device__ inline uint32_t x_find(const XEntry* __restrict__ tab, uint64_t mask, tb_uint128_t id) {
-  if ((id.lo | id.hi) == 0) return NONE32;
-  uint64_t h = hash_id(id.lo, id.hi) & mask;
+// Continues a transfer-id probe whose first entry `e` (at h & mask) is already loaded.
+__device__ inline uint32_t x_probe_from(const XEntry* __restrict__ tab, const tb_transfer_t* __restrict__ xr,
+                                        uint64_t mask, uint64_t h, XEntry e, tb_uint128_t id) {
+  const uint32_t fp = (uint32_t)(h >> 32);
+  uint64_t pos = h & mask;
   for (;;) {
-    const XEntry e = tab[h];
-    if (e.slot == NONE32) return NONE32;
-    if (e.id_lo == id.lo && e.id_hi == id.hi) return e.slot;
-    h = (h + 1) & mask;
+    if (e == X_EMPTY) return NONE32;
+    if ((uint32_t)(e >> 32) == fp) {
+      const tb_uint128_t k = xr[(uint32_t)e].id;
+      if (k.lo == id.lo && k.hi == id.hi) return (uint32_t)e;
+    }
+    pos = (pos + 1) & mask;
+    e = tab[pos];
   }
 }
+
+__device__ inline uint32_t x_find(const XEntry* __restrict__ tab, const tb_transfer_t* __restrict__ xr, uint64_t mask,
+                                  tb_uint128_t id) {
+  if ((id.lo | id.hi) == 0) return NONE32;
+  const uint64_t h = hash_id(id.lo, id.hi);
+  return x_probe_from(tab, xr, mask, h, tab[h & mask], id);
+}
+
+// Whether `id` can be in the transfer table (x_id_max bounds every stored id).
+__device__ inline bool x_may_exist(const tb_uint128_t& id, uint64_t x_id_max) { return id.hi != 0 || id.lo <= x_id_max; }
+__device__ inline uint64_t x_id_key(const tb_uint128_t& id) { return id.hi ? ~0ull : id.lo; }
 
 // Inserts of distinct, absent keys: claim by CAS on the slot word, then publish the key. Readers
 // run in later kernels only.
@@ -214,14 +229,31 @@ __device__ inline void acc_insert(AccEntry* tab, uint64_t mask, tb_uint128_t id,
   }
 }
 
+// Inserts a distinct, absent id whose record is already stored at xr[slot] (readers run in later
+// kernels): one 64-bit CAS.
 __device__ inline void x_insert(XEntry* tab, uint64_t mask, tb_uint128_t id, uint32_t slot) {
-  uint64_t h = hash_id(id.lo, id.hi) & mask;
+  const uint64_t h = hash_id(id.lo, id.hi);
+  const XEntry v = ((unsigned long long)(uint32_t)(h >> 32) << 32) | slot;
+  uint64_t pos = h & mask;
   for (;;) {
-    if (atomicCAS(&tab[h].slot, NONE32, slot) == NONE32) {
-      tab[h].id_lo = id.lo;
-      tab[h].id_hi = id.hi;
-      return;
-    }
-    h = (h + 1) & mask;
+    if (atomicCAS(&tab[pos], X_EMPTY, v) == X_EMPTY) return;
+    pos = (pos + 1) & mask;
   }
+}
+
+// Block-wide max of a u64 (one LDS word per wave), result valid in every thread.
+template <int NWAVES>
+__device__ inline unsigned long long block_max_u64(unsigned long long v, unsigned long long* lds) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(v, o, 64);
+    v = y > v ? y : v;
+  }
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  unsigned long long m = 0;
+#pragma unroll
+  for (int k = 0; k < NWAVES; k++) m = lds[k] > m ? lds[k] : m;
+  __syncthreads();
+  return m;
 }

@@ -54,15 +54,6 @@ __device__ inline uint32_t acc_probe_from(const AccEntry* __restrict__ tab, uint
     e = tab[h];
   }
 }
-__device__ inline uint32_t x_probe_from(const XEntry* __restrict__ tab, uint64_t mask, uint64_t h, XEntry e,
-                                        tb_uint128_t id) {
-  for (;;) {
-    if (e.slot == NONE32) return NONE32;
-    if (e.id_lo == id.lo && e.id_hi == id.hi) return e.slot;
-    h = (h + 1) & mask;
-    e = tab[h];
-  }
-}
 
 // A window may hold several batches only if no pulse can fall due inside it: live expiry entries
 // are >= pulse_next, and entries created inside the window expire >= its first timestamp + 1 s.
@@ -103,6 +94,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   __syncthreads();
   u128 amount_upper = 0;
   if (i < w.E) {
+    const uint64_t x_id_max = d.g->x_id_max;
     tb_transfer_t t = ev[i];
     const uint8_t* evb = reinterpret_cast<const uint8_t*>(ev);
     const uint32_t b = win_batch(w, i);
@@ -127,13 +119,15 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
           cls |= C_STATIC;
         } else {
           cls |= C_REACH;
-          const uint64_t hx = hash_id(t.id.lo, t.id.hi) & d.x_mask;
-          const uint64_t hp = hash_id(t.pending_id.lo, t.pending_id.hi) & d.x_mask;
-          const XEntry ex = d.x_tab[hx], ep = d.x_tab[hp];
+          const uint64_t hx = hash_id(t.id.lo, t.id.hi);
+          const uint64_t hp = hash_id(t.pending_id.lo, t.pending_id.hi);
+          const bool mx = x_may_exist(t.id, x_id_max), mp = x_may_exist(t.pending_id, x_id_max);
+          const XEntry ex = mx ? d.x_tab[hx & d.x_mask] : X_EMPTY;
+          const XEntry ep = mp ? d.x_tab[hp & d.x_mask] : X_EMPTY;
           id_ent = bmap_claim(s.bmap, s.bmask, evb, t.id, i, 0, epoch);
           pid_ent = bmap_claim(s.bmap, s.bmask, evb, t.pending_id, i, 1, epoch);
-          id_tslot = x_probe_from(d.x_tab, d.x_mask, hx, ex, t.id);
-          p_tslot = x_probe_from(d.x_tab, d.x_mask, hp, ep, t.pending_id);
+          id_tslot = x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id);
+          p_tslot = x_probe_from(d.x_tab, d.xr, d.x_mask, hp, ep, t.pending_id);
           if (p_tslot == NONE32) {
             code = TB_CT_PENDING_TRANSFER_NOT_FOUND;  // unless created in-window (then U)
           } else {
@@ -165,9 +159,9 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
           // Three independent probes in flight together.
           const uint64_t hd = hash_id(t.debit_account_id.lo, t.debit_account_id.hi) & d.acc_mask;
           const uint64_t hc = hash_id(t.credit_account_id.lo, t.credit_account_id.hi) & d.acc_mask;
-          const uint64_t hx = hash_id(t.id.lo, t.id.hi) & d.x_mask;
+          const uint64_t hx = hash_id(t.id.lo, t.id.hi);
           const AccEntry ed = d.acc_tab[hd], ec = d.acc_tab[hc];
-          const XEntry ex = d.x_tab[hx];
+          const XEntry ex = x_may_exist(t.id, x_id_max) ? d.x_tab[hx & d.x_mask] : X_EMPTY;
           AccEntry de, ce;
           dr_slot = acc_probe_from(d.acc_tab, d.acc_mask, hd, ed, t.debit_account_id, &de);
           cr_slot = acc_probe_from(d.acc_tab, d.acc_mask, hc, ec, t.credit_account_id, &ce);
@@ -185,7 +179,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
             const bool bal = f & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT);
             amount_upper = U(t.amount);
             if (bal && amount_upper == 0) amount_upper = (u128)0xFFFFFFFFFFFFFFFFull;
-            id_tslot = x_probe_from(d.x_tab, d.x_mask, hx, ex, t.id);
+            id_tslot = x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id);
             if (id_tslot != NONE32) {
               code = ct_exists(t, d.xr[id_tslot]);
             } else {
@@ -529,6 +523,8 @@ struct Add128 {
 template <bool XFER>
 __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w, FinalOut o) {
   __shared__ uint32_t lds[SEG / 64];
+  __shared__ unsigned long long ldsm[SEG / 64];
+  unsigned long long id_key = 0;  // this thread's inserted transfer id, for Globals::x_id_max
   const uint32_t E = w.E;
   const uint32_t i = blockIdx.x * SEG + threadIdx.x;
   uint32_t cls = 0, code = TB_CT_OK;
@@ -544,6 +540,11 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   uint32_t tot_bad, tot_ins;
   const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
   const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
+  if (XFER && ins) id_key = x_id_key(((cls & C_W) ? s.t2[i] : reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i]).id);
+  if (XFER) {
+    const unsigned long long m = block_max_u64<SEG / 64>(id_key, ldsm);
+    if (threadIdx.x == 0 && m > d.g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&d.g->x_id_max), m);
+  }
   if (i >= E) return;
   const uint64_t xbase = d.g->base;
   const uint32_t b = s.batch[i];
@@ -824,7 +825,7 @@ __global__ void __launch_bounds__(LOOKUP_THREADS) k_lookup(Dev d, const tb_uint1
         AccEntry e;
         slot[k] = acc_find(d.acc_tab, d.acc_mask, ids[i], &e);
       } else {
-        slot[k] = x_find(d.x_tab, d.x_mask, ids[i]);
+        slot[k] = x_find(d.x_tab, d.xr, d.x_mask, ids[i]);
       }
     }
     found += slot[k] != NONE32;
@@ -841,6 +842,10 @@ __global__ void __launch_bounds__(LOOKUP_THREADS) k_lookup(Dev d, const tb_uint1
   }
   if (threadIdx.x == 0) *out_count = total;
 }
+
+// Engine state initialization and flag clearing happen in kernels (see tbg_create).
+__global__ void k_init_globals(Globals* g, Globals v) { *g = v; }
+__global__ void k_clear_bits(uint32_t* p, uint32_t bits) { atomicAnd(p, ~bits); }
 
 // Harness `setup` (state_machine.zig:2545-2561).
 __global__ void k_setup(Dev d, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dpo, tb_uint128_t cp, tb_uint128_t cpo,

@@ -42,7 +42,7 @@ enum : uint32_t { SH_W_DR_LIMIT = 1, SH_W_CR_LIMIT = 2 };
 
 // Guard on every computed index of the sharded path: a violation is recorded (first one wins:
 // check id << 48 | shard-local value, in Globals::dbg[7]), the window is failed as a device error
-// (window_error bit 2) and the access is skipped. Never expected to fire.
+// (window_error bit 2, reported by tbg_sync) and the access is skipped. Never expected to fire.
 __device__ inline bool sh_guard(Globals* g, bool ok, uint32_t check, uint64_t value) {
   if (ok) return true;
   atomicCAS(reinterpret_cast<unsigned long long*>(&g->dbg[7]), 0ull,
@@ -89,7 +89,9 @@ __device__ inline uint32_t sh_claim(Globals* g, BEntry* bm, uint32_t mask, const
   }
 }
 
-// End-of-window device state (the last event's thread of k_sh_final).
+// End-of-window device state (the last event's thread of k_sh_final). Nothing written here is read
+// by k_sh_final's other blocks, which may still be running: their store base is Globals::base
+// (captured by k_sh_count) and sh_unsup is cleared by the next window's k_sh_close.
 __device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bool apply) {
   if (apply) {
     if (xfer) {
@@ -102,20 +104,16 @@ __device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bo
   }
   g->batch_amount_sum = 0;
   g->batch_huge = 0;
-  g->sh_unsup = 0;
 }
 
-// The last block of a prep launch (after every block's atomics are visible) closes the window's
-// local facts into the trailer word: capacity and overflow verdicts.
-__device__ inline void sh_prep_close(Dev d, uint4* xch, bool xfer) {
+// After prep (stream-ordered, one thread): closes the window's local facts into the trailer word,
+// capacity and overflow verdicts. (A separate launch, not a last-block pattern: no device fences in
+// the sharded kernels.)
+__global__ void k_sh_close(Dev d, uint4* xch, uint32_t xfer) {
   Globals* g = d.g;
-  __threadfence();
-  const uint32_t done = atomicAdd(&g->sh_blocks, 1u);
-  if (done != gridDim.x - 1) return;
-  __threadfence();
-  g->sh_blocks = 0;
-  const uint64_t own = __hip_atomic_load(&g->sh_own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t own = g->sh_own;
   g->sh_own = 0;
+  g->sh_unsup = 0;  // the previous window's verdict (read by every block of its k_sh_final)
   if (xfer) {
     if (g->x_count + own > d.x_max) xch[0].y = 1;
     if (window_ovf_mode(g)) xch[0].z = 1;
@@ -182,7 +180,7 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
             bool dup;
             id_ent = sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
             if (dup) atomicOr(&unsup, 1u);
-            const uint32_t xs = x_find(d.x_tab, d.x_mask, t.id);
+            const uint32_t xs = x_may_exist(t.id, d.g->x_id_max) ? x_find(d.x_tab, d.xr, d.x_mask, t.id) : NONE32;
             v.z = 1 + (xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]));
           }
         }
@@ -209,7 +207,6 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
     if (huge_any) atomicOr(&d.g->batch_huge, 1u);
     if (unsup) atomicOr(&xch[0].x, 1u);
     if (own) atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->sh_own), (unsigned long long)own);
-    sh_prep_close(d, xch, true);
   }
 }
 
@@ -261,7 +258,6 @@ __global__ void __launch_bounds__(256) k_sh_prep_ca(Dev d, Scratch s, const tb_a
   if (threadIdx.x == 0) {
     if (unsup) atomicOr(&xch[0].x, 1u);
     if (own) atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->sh_own), (unsigned long long)own);
-    sh_prep_close(d, xch, false);
   }
 }
 
@@ -326,12 +322,31 @@ __global__ void __launch_bounds__(256) k_sh_decide(Dev d, Scratch s, const uint8
   }
 }
 
+// Per-segment failure / owned-insert counts (k_wcount with the sharded boundary fences).
+__global__ void __launch_bounds__(SEG) k_sh_count(Dev d, Scratch s, uint32_t E, uint32_t xfer) {
+  __shared__ uint32_t lds[SEG / 64];
+  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
+  if (i == 0) d.g->base = xfer ? d.g->x_count : d.g->acc_count;  // k_sh_final's store base
+  uint32_t nbad = 0, nins = 0;
+  if (i < E) {
+    nbad = s.code[i] != TB_CT_OK;
+    nins = (s.cls[i] & C_INSERTED) ? 1u : 0u;
+  }
+  nbad = block_sum<SEG / 64>(nbad, lds);
+  nins = block_sum<SEG / 64>(nins, lds);
+  if (threadIdx.x == 0) {
+    s.cnt_bad[blockIdx.x] = nbad;
+    s.cnt_ins[blockIdx.x] = nins;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // final: replies (every shard) and owned effects.
 // ------------------------------------------------------------------------------------------------
 template <bool XFER>
 __global__ void __launch_bounds__(SEG) k_sh_final(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w, FinalOut o) {
   __shared__ uint32_t lds[SEG / 64];
+  __shared__ unsigned long long ldsm[SEG / 64];
   Globals* g = d.g;
   const bool unsup = __hip_atomic_load(&g->sh_unsup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   const uint32_t E = w.E;
@@ -348,13 +363,19 @@ __global__ void __launch_bounds__(SEG) k_sh_final(Dev d, Scratch s, const uint8_
   uint32_t tot_bad, tot_ins;
   const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
   const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
+  if (XFER && !unsup) {
+    const unsigned long long key =
+        (ins && i < E) ? x_id_key(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].id) : 0ull;
+    const unsigned long long m = block_max_u64<SEG / 64>(key, ldsm);
+    if (threadIdx.x == 0 && m > g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&g->x_id_max), m);
+  }
   if (i >= E) return;
   if (unsup) {
     if (i == 0) atomicOr(&g->window_error, 2u);
     if (i == E - 1) sh_window_reset(g, XFER, 0, false);
     return;
   }
-  const uint64_t xbase = XFER ? g->x_count : g->acc_count;
+  const uint64_t xbase = g->base;  // captured by k_sh_count: the last thread rewrites the count
   const uint32_t b = s.batch[i];
   if (i == w.off[b]) {
     for (int32_t bb = (int32_t)b; bb >= 0 && w.off[bb] == i; bb--) o.batch_base[bb] = rbad;

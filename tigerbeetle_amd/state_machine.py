@@ -16,9 +16,7 @@ MESSAGE_BODY_SIZE_MAX = 1048576 - 256
 
 
 def to_host(t):
-    """Device tensor -> numpy copy through pinned memory, waited for on the current stream.
-    (Pageable device->host copies were observed returning before every byte landed on this stack
-    while other streams were active)"""
+    """Device tensor -> numpy copy through pinned memory, ordered on the current stream."""
     import torch
 
     c = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
