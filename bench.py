@@ -325,7 +325,7 @@ def run_sharded(args, torch, dist, world, rank, device):
                     "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
                     "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
                     "phase_avg_us": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
-                    "exchange_bytes_per_window_per_gpu": 16 * (win * BATCH + 1)}
+                    "exchange_bytes_per_window_per_gpu": 16 + 9 * win * BATCH}
         line = {
             "metric": "committed transfers/sec (create_transfers)",
             "value": round(timed_events / elapsed, 1),

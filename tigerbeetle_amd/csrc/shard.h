@@ -9,13 +9,13 @@
 //                       debit account, the credit-account owner the credit account, the transfer-id
 //                       owner the id (pre-window `exists` comparison, :1506-1507, and in-window
 //                       duplicates through the window key map). Each writes its part of the event's
-//                       16 B exchange word; the other parts stay zero.
-//   (caller)            sum-all-reduce of the exchange words across the shards (RCCL over xGMI). Each
-//                       field has exactly one writer, so the sum is the union of the owners' parts.
+//                       9 B of exchange bytes; the other parts stay zero.
+//   (caller)            byte-wise sum all-reduce of the exchange bytes across the shards (RCCL over
+//                       xGMI). Every bit has exactly one writer, so the sum is the union of the parts.
 //   k_sh_decide  grid   every shard now holds the same per-event facts and decides every event the
 //                       same way: account lookups (:1496-1497), ledgers (:1503-1504), exists, then
 //                       linked chains (:1240-1300); identical replies on all shards.
-//   k_wcount     grid   per-segment failure / owned-insert counts.
+//   k_sh_count   grid   per-segment failure / owned-insert counts; captures the store base.
 //   k_sh_final   grid   replies, and only owned effects: the id owner appends the record and indexes the
 //                       id, the debit/credit owners add the amount (exact 128-bit atomics).
 //
@@ -23,22 +23,42 @@
 // account, no balancing), no two-phase, no in-window duplicate id, overflow-free window. Then every
 // event's outcome is a function of the owners' facts alone, and the effects commute. A window outside
 // the class is detected before anything is applied, identically on every shard (its flags travel in
-// the exchange's trailer word or follow from the reduced words), and fails with TBG_E_UNSUPPORTED at
+// the exchange's trailer or follow from the reduced bytes), and fails with TBG_E_UNSUPPORTED at
 // tbg_sync: no shard applies any of it.
 #pragma once
 #include "sm_logic.h"
 #include "walker.h"
 #include "window.h"
 
-// Exchange word per event (summed over shards; one writer per field):
-//   x: debit account's ledger (its owner; 0 = not found: an account's ledger is never 0, :1436)
-//   y: credit account's ledger
-//   z: transfer-id owner: 1 + (TB_CT_OK or the exists* code); create_accounts: 1 + the owner's code
-//   w: bit 0 debit account has debits_must_not_exceed_credits, bit 1 credit account has
-//      credits_must_not_exceed_debits (balance reads: outside the sharded class)
-// Word 0 is the trailer: x = shards that saw an unsupported event, y = shards over capacity,
-// z = shards whose overflow bound does not clear the window's amounts.
-enum : uint32_t { SH_W_DR_LIMIT = 1, SH_W_CR_LIMIT = 2 };
+// Exchange bytes of a window of E events (summed byte-wise over the shards: every bit has exactly
+// one writer, so the byte sum is the union with no carries; one uint8 all-reduce):
+//   [0, 16)         trailer, 4 x u32: shards that saw an unsupported event, shards over capacity,
+//                   shards whose overflow bound does not clear the window's amounts, unused
+//   create_transfers:
+//   [16, 16+4E)     debit account's ledger (its owner; 0 = not found: a live ledger is never 0, :1436)
+//   [16+4E, 16+8E)  credit account's ledger
+//   [16+8E, 16+9E)  bits 0-5: 1 + (TB_CT_OK or the exists* code), by the transfer-id owner;
+//                   bit 6: the debit account has debits_must_not_exceed_credits (its owner);
+//                   bit 7: the credit account has credits_must_not_exceed_debits (its owner)
+//   create_accounts:
+//   [16, 16+E)      bits 0-5: 1 + the id owner's code
+enum : uint32_t { SH_Z_MASK = 0x3F, SH_DR_LIMIT = 0x40, SH_CR_LIMIT = 0x80 };
+
+struct XchView {
+  uint32_t* trailer;
+  uint32_t *drl, *crl;  // transfers only
+  uint8_t* zw;
+};
+__host__ __device__ inline uint64_t xch_bytes(bool xfer, uint32_t E) { return 16 + (xfer ? 9ull : 1ull) * E; }
+__host__ __device__ inline XchView xch_view(void* base, uint32_t E, bool xfer) {
+  uint8_t* p = reinterpret_cast<uint8_t*>(base);
+  XchView v;
+  v.trailer = reinterpret_cast<uint32_t*>(p);
+  v.drl = xfer ? reinterpret_cast<uint32_t*>(p + 16) : nullptr;
+  v.crl = xfer ? reinterpret_cast<uint32_t*>(p + 16 + 4ull * E) : nullptr;
+  v.zw = p + 16 + (xfer ? 8ull * E : 0ull);
+  return v;
+}
 
 // Guard on every computed index of the sharded path: a violation is recorded (first one wins:
 // check id << 48 | shard-local value, in Globals::dbg[7]), the window is failed as a device error
@@ -109,16 +129,16 @@ __device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bo
 // After prep (stream-ordered, one thread): closes the window's local facts into the trailer word,
 // capacity and overflow verdicts. (A separate launch, not a last-block pattern: no device fences in
 // the sharded kernels.)
-__global__ void k_sh_close(Dev d, uint4* xch, uint32_t xfer) {
+__global__ void k_sh_close(Dev d, uint32_t* trailer, uint32_t xfer) {
   Globals* g = d.g;
   const uint64_t own = g->sh_own;
   g->sh_own = 0;
   g->sh_unsup = 0;  // the previous window's verdict (read by every block of its k_sh_final)
   if (xfer) {
-    if (g->x_count + own > d.x_max) xch[0].y = 1;
-    if (window_ovf_mode(g)) xch[0].z = 1;
+    if (g->x_count + own > d.x_max) trailer[1] = 1;
+    if (window_ovf_mode(g)) trailer[2] = 1;
   } else {
-    if (g->acc_count + own > d.acc_max) xch[0].y = 1;
+    if (g->acc_count + own > d.acc_max) trailer[1] = 1;
   }
 }
 
@@ -126,7 +146,7 @@ __global__ void k_sh_close(Dev d, uint4* xch, uint32_t xfer) {
 // create_transfers: prep
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
-                                                    uint32_t epoch, uint4* xch, uint32_t G, uint32_t me) {
+                                                    uint32_t epoch, XchView xch, uint32_t G, uint32_t me) {
   __shared__ u128 red[256];
   __shared__ uint32_t huge_any, unsup, own;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -138,7 +158,7 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
     tb_transfer_t t = ev[i];
     const uint32_t b = win_batch(w, i);
     uint32_t cls = 0, code, dr_slot = NONE32, cr_slot = NONE32, id_ent = NONE32;
-    uint4 v = make_uint4(0, 0, 0, 0);
+    uint32_t drl = 0, crl = 0, zw = 0;
     const uint16_t f = t.flags;
     if (f & TB_TRANSFER_LINKED) cls |= C_LINKED;
     if (t.timestamp != 0) {
@@ -162,16 +182,16 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
             AccEntry e;
             dr_slot = acc_find(d.acc_tab, d.acc_mask, t.debit_account_id, &e);
             if (dr_slot != NONE32) {
-              v.x = e.ledger;
-              if (e.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) v.w |= SH_W_DR_LIMIT;
+              drl = e.ledger;
+              if (e.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) zw |= SH_DR_LIMIT;
             }
           }
           if (shard_of(t.credit_account_id.lo, t.credit_account_id.hi, G) == me) {
             AccEntry e;
             cr_slot = acc_find(d.acc_tab, d.acc_mask, t.credit_account_id, &e);
             if (cr_slot != NONE32) {
-              v.y = e.ledger;
-              if (e.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) v.w |= SH_W_CR_LIMIT;
+              crl = e.ledger;
+              if (e.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) zw |= SH_CR_LIMIT;
             }
           }
           if (shard_of(t.id.lo, t.id.hi, G) == me) {
@@ -181,7 +201,7 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
             id_ent = sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
             if (dup) atomicOr(&unsup, 1u);
             const uint32_t xs = x_may_exist(t.id, d.g->x_id_max) ? x_find(d.x_tab, d.xr, d.x_mask, t.id) : NONE32;
-            v.z = 1 + (xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]));
+            zw |= 1 + (xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]));
           }
         }
       }
@@ -193,7 +213,9 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
     s.dr_slot[i] = dr_slot;
     s.cr_slot[i] = cr_slot;
     s.id_ent[i] = id_ent;
-    xch[1 + i] = v;
+    xch.drl[i] = drl;
+    xch.crl[i] = crl;
+    xch.zw[i] = (uint8_t)zw;
   }
   if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&huge_any, 1u);
   red[threadIdx.x] = ((uint64_t)(amount_upper >> 64) != 0) ? 0 : amount_upper;
@@ -205,7 +227,7 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
   if (threadIdx.x == 0) {
     if (red[0]) atomic_add_u128(reinterpret_cast<tb_uint128_t*>(&d.g->batch_amount_sum), red[0]);
     if (huge_any) atomicOr(&d.g->batch_huge, 1u);
-    if (unsup) atomicOr(&xch[0].x, 1u);
+    if (unsup) atomicOr(&xch.trailer[0], 1u);
     if (own) atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->sh_own), (unsigned long long)own);
   }
 }
@@ -214,7 +236,7 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
 // create_accounts: prep
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_sh_prep_ca(Dev d, Scratch s, const tb_account_t* __restrict__ ev, WinDesc w,
-                                                    uint32_t epoch, uint4* xch, uint32_t G, uint32_t me) {
+                                                    uint32_t epoch, XchView xch, uint32_t G, uint32_t me) {
   __shared__ uint32_t unsup, own;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (threadIdx.x == 0) unsup = own = 0;
@@ -223,8 +245,7 @@ __global__ void __launch_bounds__(256) k_sh_prep_ca(Dev d, Scratch s, const tb_a
   if (i < w.E) {
     const tb_account_t a = ev[i];
     const uint32_t b = win_batch(w, i);
-    uint32_t cls = 0, code, id_ent = NONE32;
-    uint4 v = make_uint4(0, 0, 0, 0);
+    uint32_t cls = 0, code, id_ent = NONE32, zw = 0;
     if (a.flags & TB_ACCOUNT_LINKED) cls |= C_LINKED;
     if (a.timestamp != 0) {
       cls |= C_TSNZ;
@@ -241,7 +262,7 @@ __global__ void __launch_bounds__(256) k_sh_prep_ca(Dev d, Scratch s, const tb_a
           if (dup) atomicOr(&unsup, 1u);
           AccEntry e;
           const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, a.id, &e);
-          v.z = 1 + (slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(a, d.acc[slot]));
+          zw = 1 + (slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(a, d.acc[slot]));
         }
       }
     }
@@ -252,11 +273,11 @@ __global__ void __launch_bounds__(256) k_sh_prep_ca(Dev d, Scratch s, const tb_a
     s.id_ent[i] = id_ent;
     s.dr_slot[i] = NONE32;
     s.cr_slot[i] = NONE32;
-    xch[1 + i] = v;
+    xch.zw[i] = (uint8_t)zw;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (unsup) atomicOr(&xch[0].x, 1u);
+    if (unsup) atomicOr(&xch.trailer[0], 1u);
     if (own) atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->sh_own), (unsigned long long)own);
   }
 }
@@ -265,30 +286,29 @@ __global__ void __launch_bounds__(256) k_sh_prep_ca(Dev d, Scratch s, const tb_a
 // decide: every shard, every event, from the reduced exchange words.
 // ------------------------------------------------------------------------------------------------
 template <bool XFER>
-__device__ inline uint32_t sh_code(const Dev& d, const Scratch& s, const uint8_t* ev, const uint4* xch, uint32_t j) {
+__device__ inline uint32_t sh_code(const Dev& d, const Scratch& s, const uint8_t* ev, const XchView& xch, uint32_t j) {
   const uint32_t code = s.code[j];
   if (code != CONT) return code;
-  const uint4 v = xch[1 + j];
-  if (!XFER) return v.z - 1;
-  if (v.x == 0) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;  // :1496-1497
-  if (v.y == 0) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
-  if (v.x != v.y) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;  // :1503-1504
-  if (reinterpret_cast<const tb_transfer_t*>(ev)[j].ledger != v.x)
+  const uint32_t zw = xch.zw[j];
+  const uint32_t z = (zw & SH_Z_MASK) - 1;
+  if (!XFER) return z;
+  const uint32_t drl = xch.drl[j], crl = xch.crl[j];
+  if (drl == 0) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;  // :1496-1497
+  if (crl == 0) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
+  if (drl != crl) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;  // :1503-1504
+  if (reinterpret_cast<const tb_transfer_t*>(ev)[j].ledger != drl)
     return TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
-  if (v.z - 1 != TB_CT_OK) return v.z - 1;  // exists* (:1506-1507)
+  if (z != TB_CT_OK) return z;  // exists* (:1506-1507)
   // Reaches the balance checks: overflow cannot fail in a class window; a limit flag on either
   // account is a balance read (:1546-1547), outside the class.
-  if (v.w) atomicOr(&d.g->sh_unsup, 1u);
+  if (zw & (SH_DR_LIMIT | SH_CR_LIMIT)) atomicOr(&d.g->sh_unsup, 1u);
   return TB_CT_OK;
 }
 
 template <bool XFER>
-__global__ void __launch_bounds__(256) k_sh_decide(Dev d, Scratch s, const uint8_t* ev, WinDesc w, const uint4* xch) {
+__global__ void __launch_bounds__(256) k_sh_decide(Dev d, Scratch s, const uint8_t* ev, WinDesc w, XchView xch) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) {
-    const uint4 t = xch[0];
-    if (t.x | t.y | t.z) atomicOr(&d.g->sh_unsup, 1u);
-  }
+  if (i == 0 && (xch.trailer[0] | xch.trailer[1] | xch.trailer[2])) atomicOr(&d.g->sh_unsup, 1u);
   if (i >= w.E) return;
   const uint32_t b = s.batch[i];
   const uint32_t first = w.off[b], last = w.off[b + 1] - 1;

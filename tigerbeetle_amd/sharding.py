@@ -5,8 +5,9 @@ Every shard receives the same prepared window (the replica hands each GPU the sa
 state_machine.zig:1107-1146) and commits it in three steps through the C ABI (include/tbg.h):
 
   tbg_shard_prepare_window   validate; resolve the owned accounts / ids; write exchange words
-  exchange                   element-wise int32 sum of the exchange words across the shards, on the
-                             engine's stream (RCCL all-reduce over xGMI: torch.distributed "nccl")
+  exchange                   byte-wise sum of the exchange bytes across the shards (9 B per transfer:
+                             debit / credit ledger, exists code + limit bits; one writer per bit), on
+                             the engine's stream (RCCL uint8 all-reduce over xGMI: torch "nccl")
   tbg_shard_commit_window    decide every event (identically on every shard); owned effects only
 
 The `exchange` callable is the only collective on the data path; with one shard there is none.
@@ -61,7 +62,7 @@ def exchange_gloo(t):
 
 
 class ShardedStateMachine:
-    """One shard of a hash-sharded engine. `exchange(t)` must sum the int32 tensor `t` in place
+    """One shard of a hash-sharded engine. `exchange(t)` must sum the uint8 tensor `t` in place
     across all shards (None for a single shard)."""
 
     def __init__(self, shard_count, shard_index, exchange=None, device=0, batch_max=8190, accounts_max=1 << 16,
@@ -74,7 +75,7 @@ class ShardedStateMachine:
         self.shard_count, self.shard_index = shard_count, shard_index
         self.exchange = exchange
         events_max = window_events_max or batch_max
-        self.xch = torch.zeros((events_max + 1) * 4, dtype=torch.int32, device=torch.device("cuda", device))
+        self.xch = torch.zeros(16 + 9 * events_max, dtype=torch.uint8, device=torch.device("cuda", device))
         self.stream = torch.cuda.ExternalStream(self.sm.stream, device=torch.device("cuda", device))
         torch.cuda.synchronize(device)
 
@@ -91,7 +92,8 @@ class ShardedStateMachine:
         ts = (ctypes.c_uint64 * nb)(*batch_timestamps)
         _lib.check(_lib.lib().tbg_shard_prepare_window(self.sm.h, int(operation), d_events, nb, ev, ts,
                                                        self.xch.data_ptr()), "shard_prepare_window")
-        return self.xch[: 4 * (sum(batch_events) + 1)]
+        n = _lib.lib().tbg_shard_exchange_bytes(int(operation), sum(batch_events))
+        return self.xch[:n]
 
     def commit_prepared(self, d_results, d_batch_base):
         _lib.check(_lib.lib().tbg_shard_commit_window(self.sm.h, self.xch.data_ptr(), d_results, d_batch_base),
