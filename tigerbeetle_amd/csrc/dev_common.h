@@ -103,6 +103,8 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t cc_count;    // components of W
   uint32_t cpw_done;    // the component walkers decided every W event
   uint64_t cpw_events_total;  // cumulative W events decided by component walkers
+  uint32_t small_win;   // this window: ovf_bound + window amounts < 2^64 (set by k_walk; k_final reads it)
+  uint32_t pad3;
   uint64_t x_id_max;    // >= every stored transfer id (u64 max once any id needs > 64 bits): an id
                         // above it cannot exist, so its table probe is skipped (monotonic ids)
   // sharded engines (shard.h), per window

@@ -28,6 +28,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <new>
 #include <vector>
 
@@ -438,7 +439,14 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
                                                         uint32_t nseg, uint32_t epoch) {
   __shared__ uint32_t lds[WALK_THREADS / 64];
   __shared__ uint32_t sbad[MAX_SEGS], sins[MAX_SEGS];
-  if (threadIdx.x == 0) d.g->base = XFER ? d.g->x_count : d.g->acc_count;
+  if (threadIdx.x == 0) {
+    Globals* g = d.g;
+    g->base = XFER ? g->x_count : g->acc_count;
+    // Every balance field <= ovf_bound; if ovf_bound + Σ window amounts < 2^64, no field leaves its
+    // low word during the window, so k_final's commutative adds are exact as 64-bit adds.
+    const u128 sum = g->ovf_bound + g->batch_amount_sum;
+    g->small_win = XFER && !g->batch_huge && sum >= g->ovf_bound && (uint64_t)(sum >> 64) == 0;
+  }
   uint32_t v = 0;
   for (uint32_t j = threadIdx.x; j < nseg; j += WALK_THREADS) v += s.cnt_w[j];
   const uint32_t w_count = block_sum<WALK_THREADS / 64>(v, lds);
@@ -499,34 +507,109 @@ struct FinalOut {
   tb_create_result_t* results;  // window replies, concatenated per batch
   uint32_t* batch_base;         // [nb + 1]: batch b's replies are results[base[b] .. base[b+1])
   uint32_t* out_count;          // optional: total failures (single-batch callers)
+  uint32_t xskip;               // timing experiments only (TBG_EXPERIMENT_SKIP; results are wrong):
+                                // 1 balance atomics, 2 id-table insert, 4 record store
 };
 
 // A 128-bit atomic add split in two phases so that several can be in flight before any carry is
 // resolved: issue() adds the low word (returning the old value); finish() adds the high word plus
 // the carry out of the low word. Concurrent adds compose to the exact 128-bit sum.
 struct Add128 {
-  unsigned long long* hi;
+  unsigned long long* hi = nullptr;  // null: nothing issued
   unsigned long long lo_add, hi_add, old;
-  __device__ void issue(tb_uint128_t* p, u128 v) {
+  bool small;
+  // small: the window keeps every balance field below 2^64 (Globals::small_win), so the delta is
+  // exact as a no-return 64-bit add on the low word (negative deltas wrap mod 2^64 to the right value)
+  __device__ void issue(tb_uint128_t* p, u128 v, bool small_win) {
     unsigned long long* w = reinterpret_cast<unsigned long long*>(p);
+    small = small_win;
     hi = w + 1;
     lo_add = (unsigned long long)v;
     hi_add = (unsigned long long)(v >> 64);
+    if (small) {
+      (void)atomicAdd(w, lo_add);
+      return;
+    }
     old = atomicAdd(w, lo_add);
   }
   __device__ void finish() const {
+    if (!hi || small) return;
     const unsigned long long carry = (old + lo_add) < old ? 1ull : 0ull;
     if (hi_add + carry) atomicAdd(hi, hi_add + carry);
   }
 };
 
+// tb_transfer_t as eight 16 B words, indexed statically so the record stays in registers: q0 id,
+// q1 debit_account_id, q2 credit_account_id, q3 amount, q4 pending_id, q5 user_data_128,
+// q6 {user_data_64, user_data_32, timeout}, q7 {ledger, code | flags << 16, timestamp}.
+static_assert(offsetof(tb_transfer_t, user_data_64) == 96 && offsetof(tb_transfer_t, timeout) == 108 &&
+                  offsetof(tb_transfer_t, ledger) == 112 && offsetof(tb_transfer_t, code) == 116 &&
+                  offsetof(tb_transfer_t, flags) == 118 && offsetof(tb_transfer_t, timestamp) == 120,
+              "tb_transfer_t word layout");
+static_assert(offsetof(tb_account_t, ledger) == 112 && offsetof(tb_account_t, flags) == 118 &&
+                  offsetof(tb_account_t, timestamp) == 120,
+              "tb_account_t word layout");
+__device__ inline uint64_t rw_u64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+__device__ inline tb_uint128_t rw_u128(const uint4& q) {
+  tb_uint128_t v;
+  v.lo = rw_u64(q.x, q.y);
+  v.hi = rw_u64(q.z, q.w);
+  return v;
+}
+__device__ inline void rw_stamp(uint4* r, uint64_t ts) {
+  r[7].z = (uint32_t)ts;
+  r[7].w = (uint32_t)(ts >> 32);
+}
+// pv_record (sm_logic.h) over the words: the posting/voiding record built from event r and pending p.
+__device__ inline void rw_post_void(uint4* r, const tb_transfer_t* pending, u128 amount) {
+  const uint4* p = reinterpret_cast<const uint4*>(pending);
+  r[1] = p[1];
+  r[2] = p[2];
+  r[3] = make_uint4((uint32_t)amount, (uint32_t)((uint64_t)amount >> 32), (uint32_t)(amount >> 64),
+                    (uint32_t)(amount >> 96));
+  const uint4 p5 = p[5], p6 = p[6], p7 = p[7];
+  if ((r[5].x | r[5].y | r[5].z | r[5].w) == 0) r[5] = p5;
+  if ((r[6].x | r[6].y) == 0) {
+    r[6].x = p6.x;
+    r[6].y = p6.y;
+  }
+  if (r[6].z == 0) r[6].z = p6.z;
+  r[6].w = 0;
+  r[7].x = p7.x;
+  r[7].y = (p7.y & 0xFFFFu) | (r[7].y & 0xFFFF0000u);
+}
+
+// Wave-scope LDS ordering: this wave's LDS writes are visible to all of its lanes after the call.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Final write-out, one event per thread. The 128 B event records pass through LDS (8 KiB per wave):
+// each wave loads its 64 input records with contiguous 16 B-per-lane loads, and stores its inserted
+// records -- which own the contiguous slot range [base + first rins, +count) -- the same way, instead
+// of 8 strided 16 B accesses per lane touching 64 lines each.
 template <bool XFER>
 __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w, FinalOut o) {
   __shared__ uint32_t lds[SEG / 64];
   __shared__ unsigned long long ldsm[SEG / 64];
+  __shared__ uint4 stage[SEG * 8];  // one 128 B record per event: 128 KiB
   unsigned long long id_key = 0;  // this thread's inserted transfer id, for Globals::x_id_max
   const uint32_t E = w.E;
   const uint32_t i = blockIdx.x * SEG + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t i0 = i - lane;  // the wave's first event
+  uint4* ws = stage + (threadIdx.x >> 6) * 512;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(ev_bytes) + (size_t)i0 * 8;
+    const uint32_t nrec = i0 < E ? min(64u, E - i0) : 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+      const uint32_t k = q * 64 + lane;
+      if ((k >> 3) < nrec) ws[k] = src[k];
+    }
+  }
   uint32_t cls = 0, code = TB_CT_OK;
   bool ins = false;
   if (i < E) {
@@ -540,102 +623,124 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   uint32_t tot_bad, tot_ins;
   const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
   const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
-  if (XFER && ins) id_key = x_id_key(((cls & C_W) ? s.t2[i] : reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i]).id);
+  const uint64_t xbase = d.g->base;
+  wave_sync();
+  // this event's output record (the input record, stamped; W events carry theirs in s.t2)
+  uint4 rec[8];
+  if (XFER && (cls & C_W)) {
+    const uint4* t2 = reinterpret_cast<const uint4*>(&s.t2[i]);
+#pragma unroll
+    for (int q = 0; q < 8; q++) rec[q] = t2[q];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; q++) rec[q] = ws[lane * 8 + q];
+  }
+  if (XFER && ins) id_key = x_id_key(rw_u128(rec[0]));
   if (XFER) {
     const unsigned long long m = block_max_u64<SEG / 64>(id_key, ldsm);
     if (threadIdx.x == 0 && m > d.g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&d.g->x_id_max), m);
   }
-  if (i >= E) return;
-  const uint64_t xbase = d.g->base;
-  const uint32_t b = s.batch[i];
-  if (i == w.off[b]) {
-    // event i opens batch b and every empty batch just before it
-    for (int32_t bb = (int32_t)b; bb >= 0 && w.off[bb] == i; bb--) o.batch_base[bb] = rbad;
-  }
-  if (bad) {
-    tb_create_result_t r;
-    r.index = i - w.off[b];
-    r.result = code;
-    o.results[rbad] = r;
-  }
-  const bool wev = cls & C_W;
-  if (XFER) {
-    const tb_transfer_t* ev = reinterpret_cast<const tb_transfer_t*>(ev_bytes);
-    // Balance deltas of non-W commits: low-word atomics issued first, carries resolved after the
-    // record and table writes below.
-    Add128 adds[4];
-    int nadd = 0;
-    if (!wev && (cls & C_COMMIT)) {
-      tb_account_t* dra = &d.acc[s.dr_slot[i]];
-      tb_account_t* cra = &d.acc[s.cr_slot[i]];
-      const u128 a = s.amt[i];
-      if (cls & (C_RES_DR | C_RES_CR)) {
-        // decided by the resolver, which applied the hot side(s); only a plain single-phase or
-        // pending create reaches here
-        const bool pend = cls & C_PENDING;
-        if (!(cls & C_RES_DR)) adds[nadd++].issue(pend ? &dra->debits_pending : &dra->debits_posted, a);
-        if (!(cls & C_RES_CR)) adds[nadd++].issue(pend ? &cra->credits_pending : &cra->credits_posted, a);
-      } else if (cls & C_POSTVOID) {
-        const u128 pa = s.pamt[i];
-        adds[nadd++].issue(&dra->debits_pending, (u128)0 - pa);
-        adds[nadd++].issue(&cra->credits_pending, (u128)0 - pa);
-        if (cls & C_POST) {
-          adds[nadd++].issue(&dra->debits_posted, a);
-          adds[nadd++].issue(&cra->credits_posted, a);
-        }
-        d.xstatus[s.p_tslot[i]] = (cls & C_POST) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
-      } else if (cls & C_PENDING) {
-        adds[nadd++].issue(&dra->debits_pending, a);
-        adds[nadd++].issue(&cra->credits_pending, a);
-      } else {
-        adds[nadd++].issue(&dra->debits_posted, a);
-        adds[nadd++].issue(&cra->credits_posted, a);
-      }
+  if (i < E) {
+    const uint32_t b = s.batch[i];
+    if (i == w.off[b]) {
+      // event i opens batch b and every empty batch just before it
+      for (int32_t bb = (int32_t)b; bb >= 0 && w.off[bb] == i; bb--) o.batch_base[bb] = rbad;
     }
-    if (ins) {
-      const uint64_t slot = xbase + rins;
-      tb_transfer_t t2;
-      if (wev) {
-        t2 = s.t2[i];
-      } else {
-        t2 = ev[i];
-        t2.timestamp = win_ts(w, b, i);
-        if (cls & C_POSTVOID) t2 = pv_record(t2, d.xr[s.p_tslot[i]], s.amt[i]);
+    if (bad) {
+      tb_create_result_t r;
+      r.index = i - w.off[b];
+      r.result = code;
+      o.results[rbad] = r;
+    }
+    const bool wev = cls & C_W;
+    if (XFER) {
+      // Balance deltas of non-W commits: low-word atomics issued first, carries resolved after the
+      // record and table writes below.
+      // named slots, not an indexed array (which the compiler keeps in scratch): debit and credit
+      // side, and a post's posted pair
+      Add128 a_dr, a_cr, a_dr2, a_cr2;
+      const bool small = d.g->small_win != 0;
+      if (!wev && (cls & C_COMMIT) && !(o.xskip & 1)) {
+        tb_account_t* dra = &d.acc[s.dr_slot[i]];
+        tb_account_t* cra = &d.acc[s.cr_slot[i]];
+        const u128 a = s.amt[i];
+        if (cls & (C_RES_DR | C_RES_CR)) {
+          // decided by the resolver, which applied the hot side(s); only a plain single-phase or
+          // pending create reaches here
+          const bool pend = cls & C_PENDING;
+          if (!(cls & C_RES_DR)) a_dr.issue(pend ? &dra->debits_pending : &dra->debits_posted, a, small);
+          if (!(cls & C_RES_CR)) a_cr.issue(pend ? &cra->credits_pending : &cra->credits_posted, a, small);
+        } else if (cls & C_POSTVOID) {
+          const u128 pa = s.pamt[i];
+          a_dr.issue(&dra->debits_pending, (u128)0 - pa, small);
+          a_cr.issue(&cra->credits_pending, (u128)0 - pa, small);
+          if (cls & C_POST) {
+            a_dr2.issue(&dra->debits_posted, a, small);
+            a_cr2.issue(&cra->credits_posted, a, small);
+          }
+          d.xstatus[s.p_tslot[i]] = (cls & C_POST) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
+        } else if (cls & C_PENDING) {
+          a_dr.issue(&dra->debits_pending, a, small);
+          a_cr.issue(&cra->credits_pending, a, small);
+        } else {
+          a_dr.issue(&dra->debits_posted, a, small);
+          a_cr.issue(&cra->credits_posted, a, small);
+        }
       }
-      d.xr[slot] = t2;
-      x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
-      uint8_t st = 0;
-      if (t2.flags & TB_TRANSFER_PENDING) {
-        st = wev ? s.bstatus[i] : (uint8_t)TB_PENDING_PENDING;
-        if (t2.timeout > 0) {
-          const uint64_t expires_at = expires_at_of(t2);
-          atomicMin(reinterpret_cast<unsigned long long*>(&d.g->pulse_next), (unsigned long long)expires_at);
-          const bool visible = !(t2.timestamp >> 63) && expires_at <= TB_TIMESTAMP_MAX;
-          if (st == TB_PENDING_PENDING && visible) {
-            const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), 1ull);
-            ExpEntry e;
-            e.expires_at = expires_at;
-            e.slot = (uint32_t)slot;
-            e.pad = 0;
-            d.exp[*d.exp_cur][q] = e;
+      if (ins) {
+        const uint64_t slot = xbase + rins;
+        if (!wev) {
+          rw_stamp(rec, win_ts(w, b, i));
+          if (cls & C_POSTVOID) rw_post_void(rec, &d.xr[s.p_tslot[i]], s.amt[i]);
+        }
+        if (!(o.xskip & 2)) x_insert(d.x_tab, d.x_mask, rw_u128(rec[0]), (uint32_t)slot);
+        uint8_t st = 0;
+        if ((rec[7].y >> 16) & TB_TRANSFER_PENDING) {
+          st = wev ? s.bstatus[i] : (uint8_t)TB_PENDING_PENDING;
+          const uint32_t timeout = rec[6].w;
+          if (timeout > 0) {
+            const uint64_t ts = rw_u64(rec[7].z, rec[7].w);
+            const uint64_t expires_at = ts + (uint64_t)timeout * TB_NS_PER_S;  // expires_at_of
+            atomicMin(reinterpret_cast<unsigned long long*>(&d.g->pulse_next), (unsigned long long)expires_at);
+            const bool visible = !(ts >> 63) && expires_at <= TB_TIMESTAMP_MAX;
+            if (st == TB_PENDING_PENDING && visible) {
+              const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), 1ull);
+              ExpEntry e;
+              e.expires_at = expires_at;
+              e.slot = (uint32_t)slot;
+              e.pad = 0;
+              d.exp[*d.exp_cur][q] = e;
+            }
           }
         }
+        d.xstatus[slot] = st;
       }
-      d.xstatus[slot] = st;
-    }
-    for (int k = 0; k < nadd; k++) adds[k].finish();
-  } else {
-    const tb_account_t* ev = reinterpret_cast<const tb_account_t*>(ev_bytes);
-    if (ins) {
+      a_dr.finish();
+      a_cr.finish();
+      a_dr2.finish();
+      a_cr2.finish();
+    } else if (ins) {
       const uint64_t slot = xbase + rins;
-      tb_account_t a = ev[i];
-      a.timestamp = win_ts(w, b, i);
-      d.acc[slot] = a;
+      rw_stamp(rec, win_ts(w, b, i));
+      const uint32_t aflags = rec[7].y >> 16;
       d.hot[slot] = 0;
-      acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
-      if (a.flags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS | TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS))
+      acc_insert(d.acc_tab, d.acc_mask, rw_u128(rec[0]), (uint32_t)slot, rec[7].x, aflags);
+      if (aflags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS | TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS))
         atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->limited_accounts), 1ull);
     }
+  }
+  // Compact this wave's inserted records in LDS, then store them as one contiguous run.
+  const uint32_t r0 = __shfl(rins, 0);
+  const uint32_t nins = (uint32_t)__popcll(__ballot(ins));
+  wave_sync();
+  if (ins) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) ws[(rins - r0) * 8 + q] = rec[q];
+  }
+  wave_sync();
+  if (!(o.xskip & 4)) {
+    uint4* dst = reinterpret_cast<uint4*>(XFER ? (void*)d.xr : (void*)d.acc) + (size_t)(xbase + r0) * 8;
+    for (uint32_t k = lane; k < nins * 8; k += 64) dst[k] = ws[k];
   }
   if (i == E - 1) {
     // the window's last event: totals and window-level state

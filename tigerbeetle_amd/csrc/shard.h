@@ -414,10 +414,9 @@ __global__ void __launch_bounds__(SEG) k_sh_final(Dev d, Scratch s, const uint8_
     if ((cls & C_COMMIT) && ((drs != NONE32) | (crs != NONE32) | ins)) {
       tb_transfer_t t2 = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
       const u128 a = U(t2.amount);
-      Add128 adds[2];
-      int nadd = 0;
-      if (drs != NONE32) adds[nadd++].issue(&d.acc[drs].debits_posted, a);
-      if (crs != NONE32) adds[nadd++].issue(&d.acc[crs].credits_posted, a);
+      Add128 a_dr, a_cr;
+      if (drs != NONE32) a_dr.issue(&d.acc[drs].debits_posted, a, false);
+      if (crs != NONE32) a_cr.issue(&d.acc[crs].credits_posted, a, false);
       if (ins) {
         const uint64_t slot = xbase + rins;
         t2.timestamp = win_ts(w, b, i);
@@ -425,7 +424,8 @@ __global__ void __launch_bounds__(SEG) k_sh_final(Dev d, Scratch s, const uint8_
         x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
         d.xstatus[slot] = 0;
       }
-      for (int k = 0; k < nadd; k++) adds[k].finish();
+      a_dr.finish();
+      a_cr.finish();
     }
   } else if (ins && sh_guard(g, xbase + rins < d.acc_max, 6, xbase + rins)) {
     const uint64_t slot = xbase + rins;
