@@ -42,7 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BATCH = 8190
-PHASES = ["prep", "resolve", "classify", "wcount", "wlist", "walk", "final", "pulse"]
+PHASES = ["prep", "resolve", "classify", "wcount", "wlist", "walk", "final", "pulse", "cpw"]
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
 NS_PER_S = 1_000_000_000
 
@@ -101,6 +101,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (commit time)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-phase-timing", action="store_true")
+    p.add_argument("--resolver", default="relax", choices=["relax", "wait", "off"],
+                   help="balance-limit windows: windowed relaxation (default), wait-based walkers, walker only")
     p.add_argument("--verify", action="store_true", help="setup all ok; cfg1/cfg2: every transfer ok")
     a = p.parse_args()
     if a.config is None:
@@ -405,7 +407,8 @@ def main():
     seed = args.seed + 1000 * rank  # independent stream per shard
 
     sm = StateMachine(device=device, batch_max=BATCH, accounts_max=n_acc_total, transfers_max=n_xfer + n_setup,
-                      window_events_max=win * BATCH)
+                      window_events_max=win * BATCH,
+                      resolver={"relax": True, "wait": "wait", "off": False}[args.resolver])
     stream = sm.stream
     ext = torch.cuda.ExternalStream(stream)
 
@@ -563,7 +566,7 @@ def main():
             "dtype": "u128",
             "data": "synthetic (device-generated, seed %d)" % args.seed,
             "config": {"workload": desc, "batch": BATCH, "window_batches": win, "accounts_per_gpu": n_acc,
-                       "transfers_per_gpu": n_xfer,
+                       "transfers_per_gpu": n_xfer, "resolver": args.resolver,
                        "parallelism": "independent account shards" if world > 1 else "single GPU"},
             "results": {"failed_events_timed": int(all_fails),
                         "ok_events_per_s": round((all_events - all_fails) / elapsed, 1),

@@ -40,6 +40,9 @@ typedef struct tbg_config {
 #define TBG_FLAG_NO_RESOLVER 1u
 /* Walk W events on the single sequential walker only (no component-parallel walkers). */
 #define TBG_FLAG_NO_COMPONENTS 2u
+/* Resolve balance-limit windows with the wait-based account walkers (resolver.h) instead of the
+   default windowed relaxation (relax.h). Same results; kept for comparison. */
+#define TBG_FLAG_RES_WAIT 4u
 
 #define TBG_OK 0
 #define TBG_E_INVALID (-1)   /* input_valid() would reject the request */

@@ -1,4 +1,5 @@
-"""Account-parallel resolver (csrc/resolver.h) vs the CPU restatement and vs the sequential walker.
+"""Account-parallel resolvers (csrc/relax.h windowed relaxation, the default, and csrc/resolver.h
+wait-based walkers) vs the CPU restatement and vs the sequential walker.
 
 Streams of limit-checked transfers that hover at the limit (small funding, hot accounts, both
 limit directions, pending and posted) in multi-batch windows: identical per-batch replies and final
@@ -85,10 +86,19 @@ def _run(resolver, seed, n_acc, win, bm, n_windows, pending_pct, zipf_s, amount_
     (2, 200, 8, 1024, 30, 1.2, 1000),   # pending debits/credits mixed in
     (3, 2000, 16, 8190, 10, 1.1, 5000), # many accounts, long hot lists (multi-step walks)
     (4, 20, 2, 8190, 50, 0.5, 50),      # few accounts, everything hot, near-uniform
+    (5, 100, 4, 2048, 20, 1.2, 1 << 61), # window amount sums above 2^62: 128-bit walker steps
 ])
-def test_resolver_matches_oracle_and_walker(seed, n_acc, win, bm, pending_pct, zipf_s, amount_max):
+def test_resolver_matches_oracle_and_walker(seed, n_acc, win, bm, pending_pct, zipf_s, amount_max, monkeypatch):
     rep_r, st_r = _run(True, seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
     assert st_r["resolver_events"] > 0
+    rep_x, st_x = _run("wait", seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
+    assert st_x["resolver_events"] > 0
+    assert rep_r == rep_x
+    # relaxation windows much smaller than the commit window: many chunk advances
+    monkeypatch.setenv("TBG_RELAX_CHUNK", "200")
+    rep_c, st_c = _run(True, seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
+    assert st_c["resolver_events"] > 0
+    assert rep_r == rep_c
     rep_w, st_w = _run(False, seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
     assert st_w["resolver_events"] == 0
     assert rep_r == rep_w

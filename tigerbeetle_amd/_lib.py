@@ -37,6 +37,7 @@ class Config(ctypes.Structure):
 
 FLAG_NO_RESOLVER = 1
 FLAG_NO_COMPONENTS = 2
+FLAG_RES_WAIT = 4
 
 
 class Stats(ctypes.Structure):

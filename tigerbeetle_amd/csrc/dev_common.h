@@ -99,6 +99,9 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t res_events_total;  // cumulative W events decided by the resolver
   uint64_t limited_accounts;  // accounts created with a balance-limit flag (cumulative)
   uint64_t dbg[8];            // resolver instrumentation (tbg_debug_counters)
+  uint32_t res_bar[8];        // relax.h grid barrier: per-group arrivals (zeroed per window)
+  uint32_t res_bar_top;       // groups arrived
+  uint32_t res_fc[3];         // first changed event position per iteration (rotating)
   // component-parallel walker (cpw.h), per window; reset by k_final's last event
   uint32_t cc_count;    // components of W
   uint32_t cpw_done;    // the component walkers decided every W event

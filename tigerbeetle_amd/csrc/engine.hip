@@ -39,6 +39,7 @@
 #include "sm_logic.h"
 #include "walker.h"
 #include "resolver.h"
+#include "relax.h"
 #include "window.h"
 
 // Probe continuation after a first entry was already loaded (lets the first probes of several

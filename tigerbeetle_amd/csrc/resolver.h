@@ -55,10 +55,12 @@ enum : uint32_t {
 
 struct __attribute__((aligned(16))) RState {
   uint32_t start, end, pos, slot;
-  __int128 A;  // available balance before entry `pos` (see header)
+  __int128 A;  // available balance before entry `pos` (see header); relax.h: before entry 0
   u128 d[4];   // committed effects so far: debits_pending, debits_posted, credits_pending, credits_posted
+  uint32_t dirty[2];  // relax.h: first entry whose other-side input changed, by iteration parity
+  uint32_t pad[2];
 };
-static_assert(sizeof(RState) == 96, "RState");
+static_assert(sizeof(RState) == 112, "RState");
 
 __device__ inline bool acc_is_dc(uint16_t flags) { return flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS; }
 __device__ inline uint32_t rm_field(uint32_t meta) {
@@ -85,7 +87,14 @@ __global__ void __launch_bounds__(256) k_res_keys(Dev d, Scratch s, uint32_t E, 
     s.rstate[i].start = 0;
     s.rstate[i].end = 0;
   }
+  if (i < 8) g->res_bar[i] = 0;
+  if (i == 0) {
+    g->res_bar_top = 0;
+    g->res_fc[0] = NONE32;
+  }
   if (i >= E) return;
+  s.kidx[2 * i] = NONE32;
+  s.kidx[2 * i + 1] = NONE32;
   s.st[i] = 0;
   uint32_t key[2] = {RES_DUMMY, RES_DUMMY};
   if (active) {
@@ -120,6 +129,9 @@ __global__ void __launch_bounds__(256) k_res_segs(Dev d, Scratch s, uint32_t n) 
   const bool check = side ? need_cr : need_dr;
   const bool add = !check && !pending && (side ? dc : !dc);
   const bool wait = side ? need_dr : need_cr;
+  s.kidx[v] = k;
+  s.rown[k] = 2u;
+  s.roth[k] = 1u;
   s.rmeta[k] = e | (side ? RM_SIDE : 0) | (check ? RM_CHECK : 0) | (wait ? RM_WAIT : 0) | (add ? RM_ADD : 0) |
                (pending ? RM_PEND : 0);
   s.ramt[k] = s.amt[e];
@@ -132,6 +144,7 @@ __global__ void __launch_bounds__(256) k_res_segs(Dev d, Scratch s, uint32_t n) 
     rs.slot = slot;
     rs.A = dc ? cpo - dp - dpo : dpo - cp - cpo;
     rs.d[0] = rs.d[1] = rs.d[2] = rs.d[3] = 0;
+    rs.dirty[0] = rs.dirty[1] = NONE32;
   }
   if (k + 1 == n || s.rkey[k + 1] != key) s.rstate[key].end = k + 1;
 }

@@ -72,6 +72,10 @@ struct Scratch {
   u128* ramt;                                 // sorted entries: amount
   struct RState* rstate;                      // per hot rank: segment, cursor, available balance
   uint32_t* st;                               // per event: published limit-check outcomes
+  __int128* racc;                             // relax.h: available balance after each sorted entry
+  uint32_t* kidx;                             // relax.h: per (event, side): its sorted entry (or NONE)
+  uint32_t *rown, *roth;                      // relax.h: per sorted entry: own / other side's check
+  uint2* rlink;                               // relax.h: per sorted entry: other side's entry and rank
   uint32_t *heavy, *light;                    // hot ranks by walker kind
   uint32_t *cc_parent, *cc_list;              // component-parallel walker (cpw.h)
   void* sort_tmp;

@@ -29,7 +29,10 @@ class StateMachine:
     def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20,
                  window_events_max=0, resolver=True, components=True, shard_count=0, shard_index=0):
         L = _lib.lib()
-        flags = (0 if resolver else _lib.FLAG_NO_RESOLVER) | (0 if components else _lib.FLAG_NO_COMPONENTS)
+        # resolver: True/"relax" = windowed relaxation (relax.h), "wait" = wait-based walkers
+        # (resolver.h), False = sequential walker only
+        flags = ((0 if resolver else _lib.FLAG_NO_RESOLVER) | (0 if components else _lib.FLAG_NO_COMPONENTS) |
+                 (_lib.FLAG_RES_WAIT if resolver == "wait" else 0))
         cfg = _lib.Config(device, batch_max, accounts_max, transfers_max, window_events_max, flags, shard_count,
                           shard_index)
         h = ctypes.c_void_p()
