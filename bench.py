@@ -67,6 +67,19 @@ CONFIGS = {
 CFG3_TREASURY, CFG3_TOP, CFG3_FUND, CFG3_FUND_ID = 1000, 1000, 1_000_000, 10**15
 
 
+def warm_phases(sm, nph):
+    """Per-phase average launch time (us) over the warmup windows, timed with every phase recording
+    events, and the roofline kernel's phase (prep or final, whichever is longer)."""
+    from tigerbeetle_amd import _lib
+    L = _lib.lib()
+    ms = (ctypes.c_double * nph)()
+    launches = (ctypes.c_uint64 * nph)()
+    L.tbg_timing_collect(sm.h, ms, launches, nph)
+    per_phase = {PHASES[p]: (ms[p] / launches[p] * 1000.0 if launches[p] else None) for p in range(nph)}
+    dom = max(("prep", "final"), key=lambda k: per_phase[k] or 0.0)
+    return per_phase, dom
+
+
 def pmc_traffic(config, kernel, events_per_launch):
     """Per-launch HBM traffic of `kernel` from the committed rocprofv3 PMC summary of this config
     (profiles/r1/pmc_<config>.json, made by tools/profile.sh + tools/pmc_summary.py: separate
@@ -273,13 +286,16 @@ def run_sharded(args, torch, dist, world, rank, device):
 
     widx = 0
     warm_windows = []
+    NPH = len(PHASES)
+    L.tbg_timing_collect(sm.h, (ctypes.c_double * NPH)(), (ctypes.c_uint64 * NPH)(), NPH)  # reset
+    L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else -1)  # warmup: every phase
     for b0 in range(0, warm, win):
         warm_windows.append(commit_range(Operation.create_transfers, d_xfer, b0, min(b0 + win, warm), n_xfer, widx))
         widx += 1
     sm.sync()
-    NPH = len(PHASES)
-    L.tbg_timing_collect(sm.h, (ctypes.c_double * NPH)(), (ctypes.c_uint64 * NPH)(), NPH)  # reset
-    L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else 1)
+    per_phase, dom = warm_phases(sm, NPH)
+    # timed region: only the roofline kernel's phase records events (two per window)
+    L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else (1 << PHASES.index(dom)))
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -311,12 +327,11 @@ def run_sharded(args, torch, dist, world, rank, device):
     if args.verify:
         assert acc_fail == 0 and fails == 0, (acc_fail, fails)
     if rank == 0:
-        per_phase = {PHASES[p]: (ms[p] / launches[p] * 1000.0 if launches[p] else None) for p in range(NPH)}
-        dom = max(("prep", "final"), key=lambda k: per_phase[k] or 0.0)
         roof = None
-        if per_phase[dom]:
-            us = per_phase[dom]
-            ev_per_launch = timed_events / max(launches[PHASES.index(dom)], 1)
+        di = PHASES.index(dom)
+        if launches[di]:
+            us = ms[di] / launches[di] * 1000.0
+            ev_per_launch = timed_events / launches[di]
             bytes_launch = int(shard_kernel_bytes(dom, G) * ev_per_launch)
             achieved = bytes_launch / (us * 1e-6) / 1e9
             kname = {"prep": "k_sh_prep_ct", "final": "k_sh_final<true>"}[dom]
@@ -326,7 +341,7 @@ def run_sharded(args, torch, dist, world, rank, device):
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
                     "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
                     "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
-                    "phase_avg_us": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
+                    "phase_avg_us_warmup": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
                     "exchange_bytes_per_window_per_gpu": 16 + 9 * win * BATCH}
         line = {
             "metric": "committed transfers/sec (create_transfers)",
@@ -469,17 +484,20 @@ def main():
 
     widx = 0
     warm_windows = []
+    NPH = len(PHASES)
+    L.tbg_timing_collect(sm.h, (ctypes.c_double * NPH)(), (ctypes.c_uint64 * NPH)(), NPH)  # reset
+    L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else -1)  # warmup: every phase
     for b0 in range(0, warm, win):
         warm_windows.append(commit_range(Operation.create_transfers, d_xfer, b0, min(b0 + win, warm), n_xfer, widx,
                                          args.tick))
         widx += 1
     _lib.check(L.tbg_sync(sm.h), "sync (warmup)")
+    per_phase, dom = warm_phases(sm, NPH)
     walker_before = sm.stats()["walker_events"]
     if dist:
         dist.barrier()
-    NPH = len(PHASES)
-    L.tbg_timing_collect(sm.h, (ctypes.c_double * NPH)(), (ctypes.c_uint64 * NPH)(), NPH)  # reset
-    L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else 1)
+    # timed region: only the roofline kernel's phase records events (two per window)
+    L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else (1 << PHASES.index(dom)))
 
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
@@ -529,12 +547,11 @@ def main():
             assert stats["transfers"] == n_xfer
 
     if rank == 0:
-        per_phase = {PHASES[p]: (ms[p] / launches[p] * 1000.0 if launches[p] else None) for p in range(NPH)}
-        dom = max(("prep", "final"), key=lambda k: per_phase[k] or 0.0)
         roof = None
-        if per_phase[dom]:
-            us = per_phase[dom]
-            ev_per_launch = timed_events / max(launches[PHASES.index(dom)], 1)
+        di = PHASES.index(dom)
+        if launches[di]:
+            us = ms[di] / launches[di] * 1000.0
+            ev_per_launch = timed_events / launches[di]
             bytes_launch = int(KERNEL_BYTES_PER_EVENT[dom] * ev_per_launch)
             achieved = bytes_launch / (us * 1e-6) / 1e9
             kname = {"prep": "k_ct_prep", "final": "k_final<true>"}[dom]
@@ -544,7 +561,7 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
                     "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
                     "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
-                    "phase_avg_us": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
+                    "phase_avg_us_warmup": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
                     "path_alg_GBs": round(640 * all_events / elapsed / 1e9 / max(world, 1), 1)}
         desc = {
             "cfg1": "cfg1: %d accounts, %d uniform create_transfers, %d/batch",

@@ -156,9 +156,11 @@ int tbg_gen_accounts(void *d_out, uint64_t first, uint64_t count, uint64_t seed,
 int tbg_gen_transfers_uniform(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
                               uint64_t id_offset, void *stream);
 
-/* Per-phase kernel timing with HIP events on the engine stream. Phases: 0 prep, 1 link,
- * 2 classify, 3 wcount, 4 wlist, 5 walk, 6 final, 7 pulse (all five pulse kernels). collect() synchronizes, returns the summed
- * milliseconds and launch counts per phase since the last collect, and resets. */
+/* Per-phase kernel timing with HIP events on the engine stream. Phases: 0 prep, 1 resolve
+ * (account-parallel resolver), 2 classify, 3 wcount, 4 wlist, 5 walk, 6 final, 7 pulse (all five
+ * pulse kernels), 8 cpw (component walkers). enable: < 0 every phase, 0 off, > 0 a bitmask of
+ * phases (each timed phase costs the stream two event records). collect() synchronizes, returns
+ * the summed milliseconds and launch counts per phase since the last collect, and resets. */
 int tbg_timing_enable(tbg_engine *engine, int enable);
 int tbg_timing_collect(tbg_engine *engine, double *ms, uint64_t *launches, uint32_t n_phases);
 

@@ -94,6 +94,10 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
   const uint32_t key = s.rkey[start];
   uint32_t len = 1;
   while (start + len < w.E && s.rkey[start + len] == key) len++;
+  // statistics (tbg_debug_counters): [5] longest component, [6] components, [7] W events walked
+  atomicMax((unsigned long long*)&g->dbg[5], (unsigned long long)len);
+  atomicAdd((unsigned long long*)&g->dbg[6], 1ull);
+  atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)len);
   Walker wk;
   wk.d = d;
   wk.s = s;
