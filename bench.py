@@ -58,7 +58,7 @@ KERNEL_BYTES_PER_EVENT = {
 
 CONFIGS = {
     "cfg1": dict(accounts=10_000, transfers=1_000_000, window=32, seed=42, tick=0),
-    "cfg2": dict(accounts=1_000_000, transfers=100_000_000, window=32, seed=44, tick=0),
+    "cfg2": dict(accounts=1_000_000, transfers=100_000_000, window=64, seed=44, tick=0),
     "cfg3": dict(accounts=1_000_000, transfers=10_000_000, window=32, seed=45, tick=0),
     "cfg4": dict(accounts=1_000_000, transfers=10_000_000, window=1, seed=46, tick=NS_PER_S),
     # per GPU (weak scaling): 100M accounts / 1B transfers at 8 GPUs
