@@ -42,6 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BATCH = 8190
+WINDOW_BATCHES_MAX = 128  # csrc/window.h MAXB: batches per commit window
 PHASES = ["prep", "resolve", "classify", "wcount", "wlist", "walk", "final", "pulse", "cpw"]
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
 NS_PER_S = 1_000_000_000
@@ -58,7 +59,7 @@ KERNEL_BYTES_PER_EVENT = {
 
 CONFIGS = {
     "cfg1": dict(accounts=10_000, transfers=1_000_000, window=32, seed=42, tick=0),
-    "cfg2": dict(accounts=1_000_000, transfers=100_000_000, window=64, seed=44, tick=0),
+    "cfg2": dict(accounts=1_000_000, transfers=100_000_000, window=128, seed=44, tick=0),
     "cfg3": dict(accounts=1_000_000, transfers=10_000_000, window=32, seed=45, tick=0),
     "cfg4": dict(accounts=1_000_000, transfers=10_000_000, window=1, seed=46, tick=NS_PER_S),
     # per GPU (weak scaling): 100M accounts / 1B transfers at 8 GPUs
@@ -232,7 +233,7 @@ def run_sharded(args, torch, dist, world, rank, device):
     G, me = world, rank
     n_acc = args.accounts * G
     total_batches = (args.transfers * G + BATCH - 1) // BATCH
-    win = max(1, min(args.window, 64))
+    win = max(1, min(args.window, WINDOW_BATCHES_MAX))
     warm = min(((args.warmup + win - 1) // win) * win, max(0, total_batches - win))
     steps = args.steps if args.steps is not None else total_batches - warm
     n_batches = min(total_batches, warm + steps)
@@ -249,7 +250,7 @@ def run_sharded(args, torch, dist, world, rank, device):
     d_xfer = torch.empty(n_xfer * 128, dtype=torch.uint8, device="cuda")
     d_res = torch.empty(win * BATCH * 8, dtype=torch.uint8, device="cuda")
     n_windows_max = (max(n_batches, (n_acc + BATCH - 1) // BATCH) + win - 1) // win + 1
-    d_base = torch.zeros(n_windows_max * 65, dtype=torch.int32, device="cuda")
+    d_base = torch.zeros(n_windows_max * (WINDOW_BATCHES_MAX + 1), dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
     _lib.check(L.tbg_gen_accounts(d_acc.data_ptr(), 0, n_acc, args.seed, 2, 1, 0, stream), "gen accounts")
     _lib.check(L.tbg_gen_transfers_uniform(d_xfer.data_ptr(), 0, n_xfer, args.seed, n_acc, 0, stream), "gen")
@@ -266,11 +267,11 @@ def run_sharded(args, torch, dist, world, rank, device):
             ns.append(n)
             ts.append(prepare_ts)
         sm.commit_window(op, d_events.data_ptr() + first_batch * BATCH * 128, ns, ts, d_res.data_ptr(),
-                         d_base.data_ptr() + widx * 65 * 4)
+                         d_base.data_ptr() + widx * (WINDOW_BATCHES_MAX + 1) * 4)
         return widx, len(ns)
 
     def failures(wins):
-        bases = to_host(d_base).reshape(-1, 65)
+        bases = to_host(d_base).reshape(-1, WINDOW_BATCHES_MAX + 1)
         return int(sum(bases[wi, nb] for wi, nb in wins))
 
     def barrier():
@@ -414,7 +415,7 @@ def main():
     n_acc_total = n_acc + (CFG3_TREASURY if cfg == "cfg3" else 0)
     n_setup = n_acc if cfg == "cfg3" else 0
     total_batches = (args.transfers + BATCH - 1) // BATCH
-    win = max(1, min(args.window, 64))
+    win = max(1, min(args.window, WINDOW_BATCHES_MAX))
     warm = min(((args.warmup + win - 1) // win) * win, max(0, total_batches - win))
     steps = args.steps if args.steps is not None else total_batches - warm
     n_batches = min(total_batches, warm + steps)
@@ -433,7 +434,7 @@ def main():
     d_setup = torch.empty(max(n_setup, 1) * 128, dtype=torch.uint8, device="cuda")
     d_res = torch.empty(max(n_xfer, n_acc_total, n_setup) * 8, dtype=torch.uint8, device="cuda")
     n_windows_max = (max(n_batches, (n_acc_total + BATCH - 1) // BATCH) + win - 1) // win + 1
-    d_base = torch.zeros(n_windows_max * 65, dtype=torch.int32, device="cuda")
+    d_base = torch.zeros(n_windows_max * (WINDOW_BATCHES_MAX + 1), dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
     if cfg == "cfg3":
         d_cdf = torch.from_numpy(workload.zipf_cdf(n_acc).view(np.int64).copy()).cuda()
@@ -463,11 +464,11 @@ def main():
             ts.append(prepare_ts)
         first_ev = first_batch * BATCH
         sm.commit_window(op, d_events.data_ptr() + first_ev * 128, ns, ts, d_res.data_ptr() + first_ev * 8,
-                         d_base.data_ptr() + widx * 65 * 4, True, ts[0])
+                         d_base.data_ptr() + widx * (WINDOW_BATCHES_MAX + 1) * 4, True, ts[0])
         return widx, len(ns)
 
     def failures(wins):
-        bases = to_host(d_base).reshape(-1, 65)
+        bases = to_host(d_base).reshape(-1, WINDOW_BATCHES_MAX + 1)
         return int(sum(bases[wi, nb] for wi, nb in wins))
 
     def commit_all(op, d_events, n_total):

@@ -88,7 +88,7 @@ int tbg_commit_device(tbg_engine *engine, uint32_t operation, uint64_t timestamp
  * with a batch-relative index. Requires that no pulse can fall due between the window's batches
  * (the device checks this; tbg_sync() then fails with TBG_E_STATE). With `auto_pulse`, the pulse
  * decision for the first batch (pulse_next <= prepare_timestamp) and the pulse run first.
- * Asynchronous on the engine stream. n_batches <= 64, total events <= window_events_max. */
+ * Asynchronous on the engine stream. n_batches <= 128, total events <= window_events_max. */
 int tbg_commit_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_batches,
                       const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_results,
                       uint32_t *d_batch_base, int auto_pulse, uint64_t prepare_timestamp);

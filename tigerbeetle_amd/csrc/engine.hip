@@ -1,6 +1,6 @@
 // engine.hip — MI355X batch-apply engine for the StateMachine commit path (libtbgpu.so).
 //
-// A commit window (window.h: 1..64 consecutive prepared batches, up to the configured event cap)
+// A commit window (window.h: 1..128 consecutive prepared batches, up to the configured event cap)
 // runs as six launches on the engine's stream:
 //
 //   k_*_prep     grid   stateless validation (state_machine.zig:1424-1439, 1465-1489, 1614-1624),

@@ -6,7 +6,7 @@
 #pragma once
 #include "dev_common.h"
 
-#define MAXB 64
+#define MAXB 128
 #define SEG 1024          // events per segment = threads per segment block (one event each)
 
 struct WinDesc {
