@@ -56,6 +56,10 @@ KERNEL_BYTES_PER_EVENT = {
     # (atomics), scratch read 40
     "final": 128 + 128 + 32 + 2 * 64 + 40,
 }
+# Windows that extend the sorted transfer prefix (ids strictly increasing above every stored id,
+# DESIGN.md §4): no transfer-id probe (the id is above every stored id), a direct 8 B key-map entry
+# instead of a claim, and no id-table insert in k_final.
+KERNEL_BYTES_PER_EVENT_PREFIX = {"prep": 128 + 2 * 32 + 8 + 72, "final": 128 + 128 + 2 * 64 + 40}
 
 CONFIGS = {
     "cfg1": dict(accounts=10_000, transfers=1_000_000, window=32, seed=42, tick=0),
@@ -553,7 +557,9 @@ def main():
         if launches[di]:
             us = ms[di] / launches[di] * 1000.0
             ev_per_launch = timed_events / launches[di]
-            bytes_launch = int(KERNEL_BYTES_PER_EVENT[dom] * ev_per_launch)
+            prefix = stats["sorted_transfers"] == stats["transfers"]  # every window extended the prefix
+            per_event = (KERNEL_BYTES_PER_EVENT_PREFIX if prefix else KERNEL_BYTES_PER_EVENT)[dom]
+            bytes_launch = int(per_event * ev_per_launch)
             achieved = bytes_launch / (us * 1e-6) / 1e9
             kname = {"prep": "k_ct_prep", "final": "k_final<true>"}[dom]
             tr = pmc_traffic(cfg, kname, ev_per_launch)
@@ -561,7 +567,7 @@ def main():
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
                     "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
-                    "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
+                    "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch, "alg_bytes_per_event": per_event, "sorted_prefix": prefix,
                     "phase_avg_us_warmup": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
                     "path_alg_GBs": round(640 * all_events / elapsed / 1e9 / max(world, 1), 1)}
         desc = {

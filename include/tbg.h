@@ -134,6 +134,7 @@ typedef struct tbg_stats {
     uint64_t walker_events;   /* of which ran on the sequential walker */
     uint64_t resolver_events; /* of which the account-parallel resolver decided */
     uint64_t component_events; /* of which component-parallel walkers decided */
+    uint64_t sorted_transfers; /* leading transfer records in the sorted id prefix (not hashed) */
 } tbg_stats;
 int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
 

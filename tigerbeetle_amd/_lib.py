@@ -44,7 +44,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("accounts", ctypes.c_uint64), ("transfers", ctypes.c_uint64),
                 ("expiry_entries", ctypes.c_uint64), ("pulse_next_timestamp", ctypes.c_uint64),
                 ("events_total", ctypes.c_uint64), ("walker_events", ctypes.c_uint64),
-                ("resolver_events", ctypes.c_uint64), ("component_events", ctypes.c_uint64)]
+                ("resolver_events", ctypes.c_uint64), ("component_events", ctypes.c_uint64),
+                ("sorted_transfers", ctypes.c_uint64)]
 
 
 _lib = None

@@ -108,6 +108,13 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t cpw_events_total;  // cumulative W events decided by component walkers
   uint32_t small_win;   // this window: ovf_bound + window amounts < 2^64 (set by k_walk; k_final reads it)
   uint32_t pad3;
+  // Sorted transfer prefix: records [0, x_sorted) have ids < 2^64, strictly increasing with the
+  // slot, and are not in the hash table (found by binary search, x_prefix_find). A window whose
+  // ids are strictly increasing and above every stored id extends it instead of hashing its inserts
+  // (monotonic ids, the form TigerBeetle recommends); the first other window freezes it.
+  uint64_t x_sorted;
+  uint32_t win_flags;   // this transfer window (k_prep_reduce): bit 0 claim-free, bit 1 extends the prefix
+  uint32_t mono_prev;   // the previous transfer window was claim-free (k_ct_prep's speculation)
   uint64_t x_id_max;    // >= every stored transfer id (u64 max once any id needs > 64 bits): an id
                         // above it cannot exist, so its table probe is skipped (monotonic ids)
   // sharded engines (shard.h), per window
@@ -211,6 +218,20 @@ __device__ inline uint32_t x_find(const XEntry* __restrict__ tab, const tb_trans
   if ((id.lo | id.hi) == 0) return NONE32;
   const uint64_t h = hash_id(id.lo, id.hi);
   return x_probe_from(tab, xr, mask, h, tab[h & mask], id);
+}
+
+// Binary search of the sorted transfer prefix [0, P) (Globals::x_sorted).
+__device__ inline uint32_t x_prefix_find(const tb_transfer_t* __restrict__ xr, uint64_t P, tb_uint128_t id) {
+  if (P == 0 || id.hi != 0) return NONE32;
+  uint64_t lo = 0, hi = P;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (xr[mid].id.lo < id.lo)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return (lo < P && xr[lo].id.lo == id.lo) ? (uint32_t)lo : NONE32;
 }
 
 // Whether `id` can be in the transfer table (x_id_max bounds every stored id).

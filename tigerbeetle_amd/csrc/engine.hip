@@ -89,17 +89,27 @@ __device__ inline void mark_hot(Dev d, uint32_t slot, uint32_t epoch) {
 __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
                                                  uint32_t epoch) {
   __shared__ u128 red[256];
-  __shared__ uint32_t huge_any;
+  __shared__ uint32_t aux;  // bit 0 huge amount, bit 1 not claim-free, bit 2 first id above every stored id
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (threadIdx.x == 0) huge_any = 0;
+  if (threadIdx.x == 0) aux = 0;
   if (i == 0) check_window(w, d.g);
   __syncthreads();
   u128 amount_upper = 0;
   if (i < w.E) {
     const uint64_t x_id_max = d.g->x_id_max;
+    const uint64_t P = d.g->x_sorted;
+    // speculation: claim-free like the previous window (k_claim_fix claims if it was not)
+    const bool spec = d.g->mono_prev != 0;
     tb_transfer_t t = ev[i];
     const uint8_t* evb = reinterpret_cast<const uint8_t*>(ev);
     const uint32_t b = win_batch(w, i);
+    {
+      // claim-free: ids strictly increasing over the window, all < 2^64, no post/void
+      bool nf = t.id.hi != 0 || (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
+      if (i > 0) nf |= !(t.id.lo > ev[i - 1].id.lo);
+      if (nf) atomicOr(&aux, 2u);
+      if (i == 0 && t.id.hi == 0 && t.id.lo > x_id_max) atomicOr(&aux, 4u);
+    }
     uint32_t cls = 0, code;
     uint32_t dr_slot = NONE32, cr_slot = NONE32, id_tslot = NONE32, p_tslot = NONE32, id_ent = NONE32,
              pid_ent = NONE32;
@@ -126,10 +136,14 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
           const bool mx = x_may_exist(t.id, x_id_max), mp = x_may_exist(t.pending_id, x_id_max);
           const XEntry ex = mx ? d.x_tab[hx & d.x_mask] : X_EMPTY;
           const XEntry ep = mp ? d.x_tab[hp & d.x_mask] : X_EMPTY;
-          id_ent = bmap_claim(s.bmap, s.bmask, evb, t.id, i, 0, epoch);
-          pid_ent = bmap_claim(s.bmap, s.bmask, evb, t.pending_id, i, 1, epoch);
+          if (!spec) {  // a post/void window is never claim-free: under speculation k_claim_fix claims
+            id_ent = bmap_claim(s.bmap, s.bmask, evb, t.id, i, 0, epoch);
+            pid_ent = bmap_claim(s.bmap, s.bmask, evb, t.pending_id, i, 1, epoch);
+          }
           id_tslot = x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id);
           p_tslot = x_probe_from(d.x_tab, d.xr, d.x_mask, hp, ep, t.pending_id);
+          if (id_tslot == NONE32 && mx) id_tslot = x_prefix_find(d.xr, P, t.id);
+          if (p_tslot == NONE32 && mp) p_tslot = x_prefix_find(d.xr, P, t.pending_id);
           if (p_tslot == NONE32) {
             code = TB_CT_PENDING_TRANSFER_NOT_FOUND;  // unless created in-window (then U)
           } else {
@@ -177,11 +191,12 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
             cls |= C_STATIC;
           } else {
             cls |= C_REACH;
-            id_ent = bmap_claim(s.bmap, s.bmask, evb, t.id, i, 0, epoch);
+            id_ent = spec ? bmap_direct(s.bmap, s.bmask, i, epoch) : bmap_claim(s.bmap, s.bmask, evb, t.id, i, 0, epoch);
             const bool bal = f & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT);
             amount_upper = U(t.amount);
             if (bal && amount_upper == 0) amount_upper = (u128)0xFFFFFFFFFFFFFFFFull;
             id_tslot = x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id);
+            if (id_tslot == NONE32 && x_may_exist(t.id, x_id_max)) id_tslot = x_prefix_find(d.xr, P, t.id);
             if (id_tslot != NONE32) {
               code = ct_exists(t, d.xr[id_tslot]);
             } else {
@@ -206,7 +221,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
         }
       }
     }
-    if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&huge_any, 1u);
+    if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&aux, 1u);
     // Hot marks: the first marker of an account this window gives it the next dense rank.
     if (cls & C_READS_DR) mark_hot(d, dr_slot, epoch);
     if (cls & C_READS_CR) mark_hot(d, cr_slot, epoch);
@@ -223,7 +238,8 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     s.pamt[i] = pamt;
     s.ins[i] = 0;
   }
-  // Window amount bound: block reduction, one 128-bit atomic per block.
+  // Window amount bound: block reduction into this block's partial (k_prep_reduce sums them; a
+  // same-address atomic per block serializes thousands of blocks on one memory-side word).
   red[threadIdx.x] = ((uint64_t)(amount_upper >> 64) != 0) ? 0 : amount_upper;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
@@ -231,10 +247,60 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    if (red[0]) atomic_add_u128(reinterpret_cast<tb_uint128_t*>(&d.g->batch_amount_sum), red[0]);
-    if (huge_any) atomicOr(&d.g->batch_huge, 1u);
+    s.blk_amt[blockIdx.x] = red[0];
+    s.blk_aux[blockIdx.x] = aux;
   }
 }
+
+// One block: folds the prep blocks' partials into Globals (window amount sum, huge flag) before
+// k_classify reads them. Sums of < 2^64 amounts over <= 2^20 events cannot wrap 128 bits.
+__device__ inline u128 block_sum_u128(u128 v, u128* lds) {
+  lds[threadIdx.x] = v;
+  __syncthreads();
+  for (uint32_t off = blockDim.x / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) lds[threadIdx.x] += lds[threadIdx.x + off];
+    __syncthreads();
+  }
+  return lds[0];
+}
+
+__global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t nblk) {
+  __shared__ u128 red[1024];
+  __shared__ uint32_t aux;
+  if (threadIdx.x == 0) aux = 0;
+  __syncthreads();
+  u128 v = 0;
+  uint32_t a = 0;
+  for (uint32_t j = threadIdx.x; j < nblk; j += 1024) {
+    v += s.blk_amt[j];
+    a |= s.blk_aux[j];
+  }
+  if (a) atomicOr(&aux, a);
+  const u128 tot = block_sum_u128(v, red);
+  if (threadIdx.x == 0) {
+    Globals* g = d.g;
+    g->batch_amount_sum += tot;
+    if (aux & 1u) g->batch_huge = 1;
+    const bool claim_free = !(aux & 2u);
+    const bool prefix = claim_free && (aux & 4u) && g->x_sorted == g->x_count;
+    g->win_flags = (claim_free ? 1u : 0u) | (prefix ? 2u : 0u);
+  }
+}
+
+// After k_prep_reduce: a window k_ct_prep treated as claim-free (speculation, Globals::mono_prev)
+// that is not gets its key-map claims here, before anything reads the map.
+__global__ void __launch_bounds__(256) k_claim_fix(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, uint32_t E,
+                                                   uint32_t epoch) {
+  if (!d.g->mono_prev || (d.g->win_flags & 1u)) return;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E) return;
+  const uint32_t cls = s.cls[i];
+  if (!(cls & C_REACH)) return;
+  const uint8_t* evb = reinterpret_cast<const uint8_t*>(ev);
+  s.id_ent[i] = bmap_claim(s.bmap, s.bmask, evb, ev[i].id, i, 0, epoch);
+  if (cls & C_POSTVOID) s.pid_ent[i] = bmap_claim(s.bmap, s.bmask, evb, ev[i].pending_id, i, 1, epoch);
+}
+
 
 // ------------------------------------------------------------------------------------------------
 // create_transfers: link
@@ -597,6 +663,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   __shared__ unsigned long long ldsm[SEG / 64];
   __shared__ uint4 stage[SEG * 8];  // one 128 B record per event: 128 KiB
   unsigned long long id_key = 0;  // this thread's inserted transfer id, for Globals::x_id_max
+  const bool prefix_win = XFER && (d.g->win_flags & 2u) != 0;  // k_prep_reduce
   const uint32_t E = w.E;
   const uint32_t i = blockIdx.x * SEG + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
@@ -639,6 +706,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   if (XFER && ins) id_key = x_id_key(rw_u128(rec[0]));
   if (XFER) {
     const unsigned long long m = block_max_u64<SEG / 64>(id_key, ldsm);
+    // a no-return atomic: the wave does not wait for it (unlike k_ct_prep's returning amount add)
     if (threadIdx.x == 0 && m > d.g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&d.g->x_id_max), m);
   }
   if (i < E) {
@@ -694,7 +762,8 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
           rw_stamp(rec, win_ts(w, b, i));
           if (cls & C_POSTVOID) rw_post_void(rec, &d.xr[s.p_tslot[i]], s.amt[i]);
         }
-        if (!(o.xskip & 2)) x_insert(d.x_tab, d.x_mask, rw_u128(rec[0]), (uint32_t)slot);
+        // records of a prefix-extending window are found by binary search (x_prefix_find)
+        if (!(o.xskip & 2) && !prefix_win) x_insert(d.x_tab, d.x_mask, rw_u128(rec[0]), (uint32_t)slot);
         uint8_t st = 0;
         if ((rec[7].y >> 16) & TB_TRANSFER_PENDING) {
           st = wev ? s.bstatus[i] : (uint8_t)TB_PENDING_PENDING;
@@ -751,6 +820,8 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     Globals* gw = d.g;
     gw->result_count = total_bad;
     if (XFER) {
+      if (prefix_win) gw->x_sorted = xbase + total_ins;
+      gw->mono_prev = gw->win_flags & 1u;
       gw->x_count = xbase + total_ins;
       const u128 sum = gw->ovf_bound + gw->batch_amount_sum;
       gw->ovf_bound = (gw->batch_huge || sum < gw->ovf_bound) ? MAX128 : sum;
@@ -932,6 +1003,7 @@ __global__ void __launch_bounds__(LOOKUP_THREADS) k_lookup(Dev d, const tb_uint1
         slot[k] = acc_find(d.acc_tab, d.acc_mask, ids[i], &e);
       } else {
         slot[k] = x_find(d.x_tab, d.xr, d.x_mask, ids[i]);
+        if (slot[k] == NONE32) slot[k] = x_prefix_find(d.xr, d.g->x_sorted, ids[i]);
       }
     }
     found += slot[k] != NONE32;

@@ -126,19 +126,43 @@ __device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bo
   g->batch_huge = 0;
 }
 
-// After prep (stream-ordered, one thread): closes the window's local facts into the trailer word,
-// capacity and overflow verdicts. (A separate launch, not a last-block pattern: no device fences in
-// the sharded kernels.)
-__global__ void k_sh_close(Dev d, uint32_t* trailer, uint32_t xfer) {
+// After prep (stream-ordered, one block): folds the prep blocks' partials (amount sums, huge /
+// unsupported bits, owned-id counts; no same-address atomics across blocks) and closes the window's
+// local facts into the trailer words: unsupported, capacity and overflow verdicts. (A separate
+// launch, not a last-block pattern: no device fences in the sharded kernels.)
+__global__ void __launch_bounds__(1024) k_sh_close(Dev d, Scratch s, uint32_t nblk, uint32_t* trailer, uint32_t xfer) {
+  __shared__ u128 red[1024];
+  __shared__ uint32_t bits;
+  __shared__ unsigned long long own_s;
+  if (threadIdx.x == 0) {
+    bits = 0;
+    own_s = 0;
+  }
+  __syncthreads();
+  u128 v = 0;
+  uint32_t a = 0;
+  unsigned long long own = 0;
+  for (uint32_t j = threadIdx.x; j < nblk; j += 1024) {
+    const uint32_t x = s.blk_aux[j];
+    a |= x & 3u;
+    own += x >> 2;
+    if (xfer) v += s.blk_amt[j];
+  }
+  if (a) atomicOr(&bits, a);
+  if (own) atomicAdd(&own_s, own);
+  const u128 tot = xfer ? block_sum_u128(v, red) : (u128)0;
+  if (threadIdx.x != 0) return;
   Globals* g = d.g;
-  const uint64_t own = g->sh_own;
   g->sh_own = 0;
   g->sh_unsup = 0;  // the previous window's verdict (read by every block of its k_sh_final)
+  if (bits & 2u) trailer[0] = 1;
   if (xfer) {
-    if (g->x_count + own > d.x_max) trailer[1] = 1;
+    g->batch_amount_sum += tot;
+    if (bits & 1u) g->batch_huge = 1;
+    if (g->x_count + own_s > d.x_max) trailer[1] = 1;
     if (window_ovf_mode(g)) trailer[2] = 1;
   } else {
-    if (g->acc_count + own > d.acc_max) trailer[1] = 1;
+    if (g->acc_count + own_s > d.acc_max) trailer[1] = 1;
   }
 }
 
@@ -200,7 +224,11 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
             bool dup;
             id_ent = sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
             if (dup) atomicOr(&unsup, 1u);
-            const uint32_t xs = x_may_exist(t.id, d.g->x_id_max) ? x_find(d.x_tab, d.xr, d.x_mask, t.id) : NONE32;
+            uint32_t xs = NONE32;
+            if (x_may_exist(t.id, d.g->x_id_max)) {
+              xs = x_find(d.x_tab, d.xr, d.x_mask, t.id);
+              if (xs == NONE32) xs = x_prefix_find(d.xr, d.g->x_sorted, t.id);
+            }
             zw |= 1 + (xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]));
           }
         }
@@ -224,11 +252,9 @@ __global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_t
     if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    if (red[0]) atomic_add_u128(reinterpret_cast<tb_uint128_t*>(&d.g->batch_amount_sum), red[0]);
-    if (huge_any) atomicOr(&d.g->batch_huge, 1u);
-    if (unsup) atomicOr(&xch.trailer[0], 1u);
-    if (own) atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->sh_own), (unsigned long long)own);
+  if (threadIdx.x == 0) {  // this block's partials (k_sh_close folds them)
+    s.blk_amt[blockIdx.x] = red[0];
+    s.blk_aux[blockIdx.x] = (huge_any ? 1u : 0u) | (unsup ? 2u : 0u) | (own << 2);
   }
 }
 
@@ -276,10 +302,7 @@ __global__ void __launch_bounds__(256) k_sh_prep_ca(Dev d, Scratch s, const tb_a
     xch.zw[i] = (uint8_t)zw;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    if (unsup) atomicOr(&xch.trailer[0], 1u);
-    if (own) atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->sh_own), (unsigned long long)own);
-  }
+  if (threadIdx.x == 0) s.blk_aux[blockIdx.x] = (unsup ? 2u : 0u) | (own << 2);  // k_sh_close folds them
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -383,9 +406,9 @@ __global__ void __launch_bounds__(SEG) k_sh_final(Dev d, Scratch s, const uint8_
   uint32_t tot_bad, tot_ins;
   const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
   const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
-  if (XFER && !unsup) {
+  if (XFER) {
     const unsigned long long key =
-        (ins && i < E) ? x_id_key(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].id) : 0ull;
+        (!unsup && ins && i < E) ? x_id_key(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].id) : 0ull;
     const unsigned long long m = block_max_u64<SEG / 64>(key, ldsm);
     if (threadIdx.x == 0 && m > g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&g->x_id_max), m);
   }

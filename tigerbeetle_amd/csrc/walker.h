@@ -38,6 +38,14 @@ __device__ inline uint32_t bmap_claim(BEntry* bm, uint32_t mask, const uint8_t* 
   }
 }
 
+// A claim-free window (ids strictly increasing, no post/void: no key can repeat) gives each event a
+// private entry past the hashed range instead of a claim: one plain store, no atomic.
+__device__ inline uint32_t bmap_direct(BEntry* bm, uint32_t mask, uint32_t idx, uint32_t epoch) {
+  const uint32_t e = mask + 1 + idx;
+  bm[e].key = ((unsigned long long)epoch << 32) | idx | (1ull << 21);
+  return e;
+}
+
 __device__ inline uint32_t bmap_idc(const BEntry* bm, uint32_t e, uint32_t epoch) {
   const unsigned long long k = bm[e].key;
   return bk_epoch(k) == epoch ? bk_idc(k) : 0;
