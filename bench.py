@@ -10,8 +10,8 @@ src/tigerbeetle/benchmark_load.zig:206-327). `--config` selects the other BASELI
         synthetic clock +1 s per batch (a pulse is due before every batch), 10M transfers
   cfg5  hash-sharded over the N GPUs (default when N > 1): 12.5M accounts and 125M uniform transfers
         per GPU (100M / 1B at N = 8), ~(N-1)/N of the transfers cross-shard; one stream for the whole
-        job, resident in every GPU's HBM; per window one RCCL all-reduce of the per-event owner facts
-        (tigerbeetle_amd/sharding.py, csrc/shard.h)
+        job, resident in every GPU's HBM; per window two RCCL all-reduces: the per-event owner facts
+        (9 B) and the home shards' commit bits (1 bit) (tigerbeetle_amd/sharding.py, csrc/shard.h)
 
 A "step" is one create_transfers batch of the stream, committed through the engine's
 device-resident C ABI in windows of --window consecutive batches (tbg_commit_window: pulse
@@ -126,6 +126,7 @@ def parse():
     if a.config is None:
         a.config = "cfg5" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "cfg2"
     c = CONFIGS[a.config]
+    a.window_set = a.window is not None
     for k in ("accounts", "transfers", "window", "seed"):
         if getattr(a, k) is None:
             setattr(a, k, c[k])
@@ -216,14 +217,18 @@ def cpu_baseline(args, seed):
 
 # Algorithmic bytes per event of the sharded kernels on one of G shards: every shard
 # reads each event and writes its exchange word and scratch; owned probes / effects are 1/G each.
-def shard_kernel_bytes(kernel, G):
+def shard_kernel_bytes(kernel, G, prefix):
+    """Algorithmic bytes per window event of the sharded scan / apply kernels (csrc/shard.h)."""
     if kernel == "prep":
-        # event 128, exchange word 16, scratch 22; owned: 2 account-table entries, id-table entry,
-        # key-map entry
-        return 128 + 16 + 22 + (2 * 32 + 32 + 16) / G
-    # final: scratch 8, replies; owned: event re-read 128, record append 128, id-table entry 32,
-    # two balance pairs read+write 2 x 64
-    return 8 + (128 + 128 + 32 + 2 * 64) / G
+        # k_sh_scan_ct: ids + amount 64, facts 9, scratch 13; the rest of the record (64) for events
+        # with an owned role (1 - (1 - 1/G)^3 of them); owned probes: 2 account-table entries 2 x 32,
+        # key-map claim 16 (fresh monotonic ids skip the transfer-id probe)
+        p_own = 1.0 - (1.0 - 1.0 / G) ** 3
+        return 64 + 9 + 13 + 64 * p_own + (2 * 32 + 16) / G
+    # k_sh_apply: roles byte + commit bit; owned: per balance side amount 16 + slot 4 + balance
+    # read+write 64, record read + append 2 x 128, id-table entry 32 unless the window extends the
+    # sorted prefix
+    return 1.125 + (2 * (16 + 4 + 64) + 256 + (0 if prefix else 32)) / G
 
 
 def run_sharded(args, torch, dist, world, rank, device):
@@ -237,7 +242,9 @@ def run_sharded(args, torch, dist, world, rank, device):
     G, me = world, rank
     n_acc = args.accounts * G
     total_batches = (args.transfers * G + BATCH - 1) // BATCH
-    win = max(1, min(args.window, WINDOW_BATCHES_MAX))
+    # N > 1: 128-batch windows (each rank is home for 128 / N of them; rehearsal at G = 8 on one GPU:
+    # 5.1G vs 3.3G transfers/s before the collectives, profiles/r1/rehearse_*.json)
+    win = max(1, min(args.window if (args.window_set or G == 1) else WINDOW_BATCHES_MAX, WINDOW_BATCHES_MAX))
     warm = min(((args.warmup + win - 1) // win) * win, max(0, total_batches - win))
     steps = args.steps if args.steps is not None else total_batches - warm
     n_batches = min(total_batches, warm + steps)
@@ -270,9 +277,9 @@ def run_sharded(args, torch, dist, world, rank, device):
             prepare_ts += 1 + n
             ns.append(n)
             ts.append(prepare_ts)
-        sm.commit_window(op, d_events.data_ptr() + first_batch * BATCH * 128, ns, ts, d_res.data_ptr(),
-                         d_base.data_ptr() + widx * (WINDOW_BATCHES_MAX + 1) * 4)
-        return widx, len(ns)
+        _, count = sm.commit_window(op, d_events.data_ptr() + first_batch * BATCH * 128, ns, ts, d_res.data_ptr(),
+                                    d_base.data_ptr() + widx * (WINDOW_BATCHES_MAX + 1) * 4)
+        return widx, count  # this rank's home batches: d_base[widx, count] = their failures
 
     def failures(wins):
         bases = to_host(d_base).reshape(-1, WINDOW_BATCHES_MAX + 1)
@@ -324,10 +331,14 @@ def run_sharded(args, torch, dist, world, rank, device):
     fails = failures(warm_windows) + timed_fails
     elapsed = wall
     if dist:
+        # each rank replied for its home batches: failures are summed, the time is the max
         dev = "cpu" if args.backend == "gloo" else "cuda"
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        f = torch.tensor([acc_fail, fails, timed_fails], dtype=torch.float64, device=dev)
+        dist.all_reduce(f, op=dist.ReduceOp.SUM)
+        acc_fail, fails, timed_fails = (int(x) for x in f.tolist())
     st = sm.stats()
     if args.verify:
         assert acc_fail == 0 and fails == 0, (acc_fail, fails)
@@ -337,9 +348,10 @@ def run_sharded(args, torch, dist, world, rank, device):
         if launches[di]:
             us = ms[di] / launches[di] * 1000.0
             ev_per_launch = timed_events / launches[di]
-            bytes_launch = int(shard_kernel_bytes(dom, G) * ev_per_launch)
+            prefix = st["sorted_transfers"] == st["transfers"]
+            bytes_launch = int(shard_kernel_bytes(dom, G, prefix) * ev_per_launch)
             achieved = bytes_launch / (us * 1e-6) / 1e9
-            kname = {"prep": "k_sh_prep_ct", "final": "k_sh_final<true>"}[dom]
+            kname = {"prep": "k_sh_scan_ct", "final": "k_sh_apply<true>"}[dom]
             tr = pmc_traffic("cfg5", kname, ev_per_launch) if G == 1 else None
             roof = {"bound": "hbm", "kernel": kname, "events_per_launch": int(ev_per_launch),
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -347,7 +359,7 @@ def run_sharded(args, torch, dist, world, rank, device):
                     "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
                     "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
                     "phase_avg_us_warmup": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
-                    "exchange_bytes_per_window_per_gpu": 16 + 9 * win * BATCH}
+                    "exchange_bytes_per_window_per_gpu": 16 + 9 * win * BATCH + 16 + win * BATCH // 8}
         line = {
             "metric": "committed transfers/sec (create_transfers)",
             "value": round(timed_events / elapsed, 1),
@@ -365,8 +377,8 @@ def run_sharded(args, torch, dist, world, rank, device):
                                    "(%.1f %% cross-shard), %d/batch" % (n_acc, G, n_xfer, 100.0 * (G - 1) / G, BATCH),
                        "batch": BATCH, "window_batches": win, "accounts_per_gpu": args.accounts,
                        "transfers_per_gpu": args.transfers,
-                       "parallelism": "hash-sharded accounts+ids, RCCL all-reduce per window" if G > 1 else
-                                      "single shard"},
+                       "parallelism": "hash-sharded accounts+ids, home batch ranges, two RCCL all-reduces "
+                                      "per window (owner facts, commit bits)" if G > 1 else "single shard"},
             "results": {"failed_events_timed": int(timed_fails),
                         "ok_events_per_s": round((timed_events - timed_fails) / elapsed, 1),
                         "shard0_accounts": st["accounts"], "shard0_transfers": st["transfers"],

@@ -102,23 +102,32 @@ void *tbg_stream(tbg_engine *engine);
 /* Hash-sharded commit over G GPUs of one node (tigerbeetle_amd/csrc/shard.h). The replacement for
  * the same commit (state_machine.zig:1220-1306) when accounts are partitioned across engines:
  * account a lives on shard tbg_shard_of(a.id), transfer t on shard tbg_shard_of(t.id). Every shard
- * receives the same window (same arguments as tbg_commit_window) and:
- *   1. tbg_shard_prepare_window: validates, resolves what it owns, writes
- *      tbg_shard_exchange_bytes(operation, E) bytes at d_exchange (16 B trailer, then per-event
- *      owner facts: 9 B per create_transfers event, 1 B per create_accounts event);
+ * receives the same window (same arguments as tbg_commit_window) and is the home of a contiguous
+ * range of its batches (it decides them and writes their replies):
+ *   1. tbg_shard_prepare_window: validates and resolves what it owns (accounts, transfer ids) and
+ *      writes tbg_shard_exchange_bytes(operation, E) bytes of owner facts at d_exchange (16 B trailer,
+ *      then 9 B per create_transfers event / 1 B per create_accounts event);
  *   2. the caller sums those bytes element-wise across all G shards in place, ordered on the engine
  *      stream (ncclAllReduce(uint8, ncclSum) over xGMI, e.g. torch.distributed.all_reduce); every bit
  *      has exactly one writer, so the byte-wise sum is exact;
- *   3. tbg_shard_commit_window: decides every event identically on every shard, writes the window's
- *      replies (as tbg_commit_window) and applies only the owned effects.
+ *   3. tbg_shard_decide_window: decides the home batches [home_first, home_first + home_count) from
+ *      the summed facts; writes their replies (d_results / d_batch_base as tbg_commit_window, for the
+ *      home batches only, d_batch_base[0..home_count]) and one commit bit per window event at
+ *      d_commit_bits (tbg_shard_commit_bits_bytes(E) bytes: 16 B trailer + E bits, zero outside the
+ *      home batches);
+ *   4. the caller sums the commit-bit bytes across the shards in place, as in 2;
+ *   5. tbg_shard_commit_window: applies only the owned effects of the committed events.
  * Sharded class: create_accounts and create_transfers without limits, balancing, two-phase or
  * in-window duplicate ids, overflow-free. Any other window is rejected whole on every shard:
  * tbg_sync returns TBG_E_UNSUPPORTED and no shard has applied it. Asynchronous on the engine stream. */
 uint32_t tbg_shard_of(uint64_t id_lo, uint64_t id_hi, uint32_t shard_count);
 uint64_t tbg_shard_exchange_bytes(uint32_t operation, uint32_t n_events);
+uint64_t tbg_shard_commit_bits_bytes(uint32_t n_events);
 int tbg_shard_prepare_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_batches,
                              const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_exchange);
-int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, void *d_results, uint32_t *d_batch_base);
+int tbg_shard_decide_window(tbg_engine *engine, const void *d_exchange, uint32_t home_first, uint32_t home_count,
+                            void *d_results, uint32_t *d_batch_base, void *d_commit_bits);
+int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, const void *d_commit_bits);
 
 /* Test hook mirroring the harness `setup` action (state_machine.zig:2545-2561). */
 int tbg_setup_balances(tbg_engine *engine, const tb_uint128_t *id, const tb_uint128_t *debits_pending,

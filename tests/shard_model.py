@@ -6,8 +6,11 @@ CPU with real torch.distributed (gloo) collectives, world size > 1, without a GP
   prep     each shard writes, per event, only the facts it owns (debit / credit account ledger and
            limit bit, transfer-id exists code) into a (1 + E) x 4 int32 word array; word 0 = trailer
   exchange element-wise sum across shards (dist.all_reduce)
-  decide   every shard decides every event identically from the summed words (+ linked chains)
-  apply    owned effects only (id owner stores the record, account owners add the amount)
+  decide   each shard decides its home batches (a contiguous range of the window's batches) from
+           the summed words (+ linked chains) and sets one commit flag per home event
+  exchange element-wise sum of the commit flags across shards
+  apply    owned effects of committed events only (id owner stores the record, account owners add
+           the amount)
 
 Validation order follows state_machine.zig:1421-1489 (create_account / create_transfer heads), the
 exists comparisons :1450-1460 and :1587-1606, chains :1240-1300. Only the sharded class is modelled
@@ -178,12 +181,12 @@ class ShardModel:
             i = end + 1
         return codes
 
-    def apply(self, op, events, codes, T, n):
+    def apply(self, op, events, commit, timestamps):
         for i, ev in enumerate(events):
-            if codes[i] != 0:
+            if not commit[i]:
                 continue
             rec = ev.copy()
-            rec["timestamp"] = T - n + i + 1
+            rec["timestamp"] = timestamps[i]
             if op == "a":
                 if self.owns(ev, "id"):
                     self.accounts[field(ev, "id")] = rec

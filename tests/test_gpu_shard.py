@@ -32,6 +32,8 @@ class LocalShards:
             s.close()
 
     def commit_window(self, op, batches, tick_ns=0):
+        """The five steps of csrc/shard.h with both exchanges summed in-process; returns the per-batch
+        replies assembled from every shard's home batches."""
         import torch
 
         self.prepare_timestamp += tick_ns
@@ -43,56 +45,39 @@ class LocalShards:
         data = np.concatenate([np.frombuffer(ev.tobytes(), np.uint8) for ev in batches])
         d_ev = torch.from_numpy(data.copy()).cuda() if len(data) else torch.zeros(128, dtype=torch.uint8).cuda()
         torch.cuda.synchronize()
-        words = [s.prepare_window(op, d_ev.data_ptr(), ns, ts) for s in self.shards]
-        for s in self.shards:  # engine streams are non-blocking: wait for each explicitly
-            s.stream.synchronize()
-        total = words[0].clone()
-        for w in words[1:]:
-            total += w
-        for w in words:
-            w.copy_(total)
-        torch.cuda.synchronize()
-        outs = []
-        for s in self.shards:
-            d_res = torch.zeros(max(sum(ns), 1) * 8, dtype=torch.uint8).cuda()
-            d_base = torch.zeros(len(ns) + 1, dtype=torch.int32).cuda()
+
+        def summed(tensors):
+            for s in self.shards:  # engine streams are non-blocking: wait for each explicitly
+                s.stream.synchronize()
+            total = tensors[0].clone()
+            for t in tensors[1:]:
+                total += t
+            for t in tensors:
+                t.copy_(total)
             torch.cuda.synchronize()
-            s.commit_prepared(d_res.data_ptr(), d_base.data_ptr())
-            outs.append((d_res, d_base))
-        for r, s in enumerate(self.shards):
-            try:
-                s.sync()
-            except RuntimeError as e:
-                if "status -3" in str(e):
-                    raise RuntimeError(f"shard {r}: {e}; {self._diagnose(r, op, batches)}") from e
-                raise
-        replies = []
-        for d_res, d_base in outs:
+
+        summed([s.prepare_window(op, d_ev.data_ptr(), ns, ts) for s in self.shards])
+        outs, bits = [], []
+        for s in self.shards:
+            first, count = s.home_range(len(ns))
+            d_res = torch.zeros(max(sum(ns), 1) * 8, dtype=torch.uint8).cuda()
+            d_base = torch.zeros(count + 1, dtype=torch.int32).cuda()
+            torch.cuda.synchronize()
+            bits.append(s.decide_window(first, count, d_res.data_ptr(), d_base.data_ptr()))
+            outs.append((first, count, d_res, d_base))
+        summed(bits)
+        for s in self.shards:
+            s.commit_decided()
+        for s in self.shards:
+            s.sync()
+        replies = [None] * len(ns)
+        for first, count, d_res, d_base in outs:
             res = to_host(d_res).tobytes()
             base = to_host(d_base)
-            replies.append([res[base[b] * 8: base[b + 1] * 8] for b in range(len(ns))])
-        assert all(r == replies[0] for r in replies[1:]), "shards disagree on the replies"
-        return replies[0]
-
-    def _diagnose(self, r, op, batches):
-        """Invariants of the failed window's per-event class bits (C_OWN 1<<18, C_INSERTED 1<<14,
-        C_COMMIT 1<<13) and codes, read back from shard r."""
-        from tigerbeetle_amd import _lib
-        from tigerbeetle_amd.sharding import shard_of
-
-        ev = np.concatenate(batches)
-        n = len(ev)
-        cls = np.zeros(n, np.uint32)
-        code = np.zeros(n, np.uint32)
-        _lib.lib().tbg_debug_last_batch(self.shards[r].h, cls.ctypes.data, code.ctypes.data, n)
-        G = len(self.shards)
-        own = shard_of(ev["id_lo"], ev["id_hi"], G) == r
-        c_own, c_ins = (cls >> 18) & 1 == 1, (cls >> 14) & 1 == 1
-        ok = code == 0
-        return (f"events {n}, C_OWN {int(c_own.sum())} (hash-owned {int(own.sum())}, mismatched "
-                f"{int((c_own != own).sum())}), C_INSERTED {int(c_ins.sum())} (owned ok {int((own & ok).sum())}, "
-                f"inserted-not-owned {int((c_ins & ~c_own).sum())}), codes not ok {int((~ok).sum())}, "
-                f"stats {self.shards[r].stats()}")
+            for k in range(count):
+                replies[first + k] = res[base[k] * 8: base[k + 1] * 8]
+        assert all(r is not None for r in replies)
+        return replies
 
     def dump_accounts(self):
         a = np.concatenate([s.sm.dump_accounts() for s in self.shards])

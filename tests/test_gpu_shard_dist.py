@@ -1,6 +1,7 @@
-"""Hash-sharded engine across processes: two ranks (one engine each, sharing cuda:0), the exchange a
+"""Hash-sharded engine across processes: two ranks (one engine each, sharing cuda:0), both exchanges a
 real torch.distributed all-reduce (gloo through pinned host memory here; RCCL on a multi-GPU node).
-Every rank's replies and the union of the ranks' stores must equal the CPU restatement's."""
+The ranks' replies (each for its home batches) and the union of their stores must equal the CPU
+restatement's."""
 import os
 import socket
 
@@ -74,14 +75,16 @@ def _rank_main(rank, world, port, seed, n_acc, n_windows, out_dir):
         d_res = torch.zeros(sum(ns) * 8, dtype=torch.uint8, device="cuda")
         d_base = torch.zeros(len(ns) + 1, dtype=torch.int32, device="cuda")
         torch.cuda.synchronize()
-        sh.commit_window(op, d_ev.data_ptr(), ns, ts, d_res.data_ptr(), d_base.data_ptr())
+        first, count = sh.commit_window(op, d_ev.data_ptr(), ns, ts, d_res.data_ptr(), d_base.data_ptr())
         sh.sync()
         res, base = to_host(d_res).tobytes(), to_host(d_base)
-        replies.append([res[base[b] * 8: base[b + 1] * 8] for b in range(len(ns))])
+        replies.append([first] + [res[base[k] * 8: base[k + 1] * 8] for k in range(count)])
     np.save(os.path.join(out_dir, f"acc{rank}.npy"), sh.sm.dump_accounts())
     np.save(os.path.join(out_dir, f"xfer{rank}.npy"), sh.sm.dump_transfers())
-    with open(os.path.join(out_dir, f"rep{rank}.bin"), "wb") as f:
-        f.write(_pack(replies))
+    import json
+
+    with open(os.path.join(out_dir, f"rep{rank}.json"), "w") as f:
+        json.dump([[w[0]] + [x.hex() for x in w[1:]] for w in replies], f)
     sh.close()
     dist.destroy_process_group()
 
@@ -103,9 +106,16 @@ def test_two_rank_gloo_matches_oracle(tmp_path):
             op = Operation.create_accounts if kind == "a" else Operation.create_transfers
             expect.append(oracle_batches(ref, op, batches))
         assert any(len(b) for w in expect[1:] for b in w)  # the stream really fails events
+        import json
+
+        got = [[None] * len(w) for w in expect]
         for r in range(world):
-            got = (tmp_path / f"rep{r}.bin").read_bytes()
-            assert got == _pack(expect), f"rank {r} replies"
+            with open(tmp_path / f"rep{r}.json") as f:
+                for wi, (first, *reps) in enumerate(json.load(f)):
+                    for k, x in enumerate(reps):
+                        assert got[wi][first + k] is None, "two homes for one batch"
+                        got[wi][first + k] = bytes.fromhex(x)
+        assert _pack(got) == _pack(expect)
         acc = np.concatenate([np.load(tmp_path / f"acc{r}.npy") for r in range(world)])
         xfer = np.concatenate([np.load(tmp_path / f"xfer{r}.npy") for r in range(world)])
         acc = acc[np.argsort(acc["timestamp"], kind="stable")]

@@ -1,6 +1,6 @@
 """CPU tests of the hash-sharded path (no GPU): the ownership hash matches the library's, and the
-sharded decomposition (owner facts -> all-reduce -> identical decide -> owned effects) reproduces the
-CPU restatement, with real gloo collectives at world size 2 and 3."""
+sharded decomposition (owner facts -> all-reduce -> home-batch decide -> all-reduce of commit flags
+-> owned effects) reproduces the CPU restatement, with real gloo collectives at world size 2 and 3."""
 import os
 import socket
 
@@ -10,6 +10,7 @@ import pytest
 from tigerbeetle_amd.sharding import shard_of
 
 BM = 64
+WINDOW_BATCHES = 3
 
 
 def test_shard_of_matches_library():
@@ -48,14 +49,16 @@ def _stream(seed, n_acc, n_batches):
     again = a[: BM].copy()
     again["user_data_64"] = rng.integers(0, 2, BM)
     out.append(("a", again))
-    next_id = 1
-    for _ in range(n_batches):
+    next_id = win_start = 1
+    for k_batch in range(n_batches):
+        if k_batch % WINDOW_BATCHES == 0:
+            win_start = next_id  # retries only of ids from earlier windows: no in-window duplicates
         n = int(rng.integers(1, BM + 1))
         t = np.zeros(n, TRANSFER_DTYPE)
         t["id_lo"] = np.arange(next_id, next_id + n, dtype=np.uint64)
-        if next_id > 200:
+        if win_start > 200:
             k = min(n // 6, 10)
-            t["id_lo"][:k] = rng.choice(np.arange(1, next_id - 1, dtype=np.uint64), k, replace=False)
+            t["id_lo"][:k] = rng.choice(np.arange(1, win_start - 1, dtype=np.uint64), k, replace=False)
         next_id += n
         dr = rng.integers(1, n_acc + 5, n)
         cr = rng.integers(1, n_acc + 5, n)
@@ -80,21 +83,51 @@ def _rank(rank, world, port, seed, n_acc, n_batches, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from shard_model import ca_static, ct_static
+    from tigerbeetle_amd.sharding import home_range
+
     m = ShardModel(world, rank)
-    T, replies = 0, []
-    for op, ev in _stream(seed, n_acc, n_batches):
-        T += 1 + len(ev)
-        words, static = m.prep(op, ev)
+    T, mine = 0, {}
+    for wi, (op, batches) in enumerate(_windows(seed, n_acc, n_batches)):
+        events = np.concatenate(batches)
+        offs, ts = np.cumsum([0] + [len(b) for b in batches]), []
+        for ev in batches:
+            T += 1 + len(ev)
+            ts += [T - len(ev) + j + 1 for j in range(len(ev))]
+        words, _ = m.prep(op, events)
         w = torch.from_numpy(words)
-        dist.all_reduce(w)  # the only collective: owner facts summed across shards
-        codes = m.decide(op, ev, w.numpy(), static)
-        m.apply(op, ev, codes, T, len(ev))
-        replies.append(np.array([(i, c) for i, c in enumerate(codes) if c != 0], np.uint32).reshape(-1, 2))
+        dist.all_reduce(w)  # exchange 1: owner facts summed across shards
+        first, count = home_range(len(batches), world, rank)
+        commit = torch.zeros(len(events), dtype=torch.int32)
+        for b in range(first, first + count):
+            ev = batches[b]
+            wb = np.concatenate([w.numpy()[:1], w.numpy()[1 + offs[b]: 1 + offs[b + 1]]])
+            static = [ca_static(e) if op == "a" else ct_static(e) for e in ev]
+            codes = m.decide(op, ev, wb, static)
+            commit[offs[b]: offs[b + 1]] = torch.tensor([c == 0 for c in codes], dtype=torch.int32)
+            mine[(wi, b)] = np.array([(i, c) for i, c in enumerate(codes) if c != 0], np.uint32).reshape(-1, 2)
+        dist.all_reduce(commit)  # exchange 2: commit flags of every home's events
+        m.apply(op, events, commit.numpy(), ts)
     np.save(os.path.join(out_dir, f"acc{rank}.npy"), np.array(list(m.accounts.values())))
     np.save(os.path.join(out_dir, f"xfer{rank}.npy"), np.array(list(m.transfers.values())))
+    keys = sorted(mine)
+    np.save(os.path.join(out_dir, f"keys{rank}.npy"), np.array(keys, np.int64).reshape(-1, 2))
     np.save(os.path.join(out_dir, f"rep{rank}.npy"), np.concatenate(
-        [np.concatenate([[[len(r), 0]], r]).astype(np.uint32) for r in replies]))
+        [np.concatenate([[[len(mine[k]), 0]], mine[k]]).astype(np.uint32) for k in keys]
+        or [np.zeros((0, 2), np.uint32)]))
     dist.destroy_process_group()
+
+
+def _windows(seed, n_acc, n_batches, per=None):
+    """The stream grouped into windows of up to `per` consecutive batches of one operation."""
+    per = per or WINDOW_BATCHES
+    out = []
+    for op, ev in _stream(seed, n_acc, n_batches):
+        if out and out[-1][0] == op and len(out[-1][1]) < per:
+            out[-1][1].append(ev)
+        else:
+            out.append((op, [ev]))
+    return out
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -112,15 +145,25 @@ def test_sharded_protocol_matches_oracle(world, tmp_path):
     mp.spawn(_rank, args=(world, port, seed, n_acc, n_batches, str(tmp_path)), nprocs=world, join=True)
     ref = OracleStateMachine(batch_max=BM)
     try:
-        parts = []
-        for op, ev in _stream(seed, n_acc, n_batches):
-            r = run_protocol(ref, Operation.create_accounts if op == "a" else Operation.create_transfers, ev)
-            rr = np.frombuffer(r, np.uint32).reshape(-1, 2)
-            parts.append(np.concatenate([[[len(rr), 0]], rr]).astype(np.uint32))
-        expect = np.concatenate(parts)
-        assert (expect[:, 1] != 0).any()
+        expect = {}
+        for wi, (op, batches) in enumerate(_windows(seed, n_acc, n_batches)):
+            for b, ev in enumerate(batches):
+                r = run_protocol(ref, Operation.create_accounts if op == "a" else Operation.create_transfers, ev)
+                expect[(wi, b)] = np.frombuffer(r, np.uint32).reshape(-1, 2)
+        assert any(len(v) for v in expect.values())
+        got = {}
         for r in range(world):
-            assert np.array_equal(np.load(tmp_path / f"rep{r}.npy"), expect), f"rank {r}"
+            keys = [tuple(k) for k in np.load(tmp_path / f"keys{r}.npy").tolist()]
+            rep = np.load(tmp_path / f"rep{r}.npy")
+            pos = 0
+            for k in keys:
+                n = int(rep[pos, 0])
+                assert k not in got, "two homes for one batch"
+                got[k] = rep[pos + 1: pos + 1 + n]
+                pos += 1 + n
+        assert sorted(got) == sorted(expect)
+        for k in expect:
+            assert np.array_equal(got[k], expect[k]), k
         acc = np.concatenate([np.load(tmp_path / f"acc{r}.npy").astype(ACCOUNT_DTYPE) for r in range(world)])
         xfer = np.concatenate([np.load(tmp_path / f"xfer{r}.npy").astype(TRANSFER_DTYPE) for r in range(world)])
         acc = acc[np.argsort(acc["timestamp"], kind="stable")]

@@ -16,7 +16,8 @@ EXPORTS = [
     "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_version", "tbg_debug_last_batch",
     "tbg_timing_enable", "tbg_timing_collect", "tbg_gen_accounts_cfg3", "tbg_gen_funding_cfg3",
     "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4", "tbg_debug_counters", "tbg_shard_of",
-    "tbg_shard_prepare_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
+    "tbg_shard_prepare_window", "tbg_shard_decide_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
+    "tbg_shard_commit_bits_bytes",
 ]
 
 
@@ -97,7 +98,9 @@ def lib():
         "tbg_debug_counters": ([vp, vp, u32], i32),
         "tbg_shard_of": ([u64, u64, u32], u32),
         "tbg_shard_prepare_window": ([vp, u32, vp, u32, vp, vp, vp], i32),
-        "tbg_shard_commit_window": ([vp, vp, vp, vp], i32),
+        "tbg_shard_decide_window": ([vp, vp, u32, u32, vp, vp, vp], i32),
+        "tbg_shard_commit_window": ([vp, vp, vp], i32),
+        "tbg_shard_commit_bits_bytes": ([u32], u64),
         "tbg_shard_exchange_bytes": ([u32, u32], u64),
     }
     for name, (args, res) in sig.items():

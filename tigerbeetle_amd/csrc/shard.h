@@ -1,30 +1,36 @@
-// shard.h — hash-sharded commit across G GPUs of one node (one engine per GPU).
+// shard.h — hash-sharded commit across G GPUs of one node (one engine per GPU), with home slices.
 //
 // Ownership: an account belongs to shard_of(account id), a transfer to shard_of(transfer id). Every
-// shard holds the whole prepared window in HBM (the replica hands each GPU the same prepare body)
-// and walks all of it, but touches state only for what it owns:
+// shard holds the whole prepared window in HBM (the replica hands each GPU the same prepare body).
+// Each shard is also the HOME of a contiguous range of the window's batches: it decides those events
+// and writes their replies. Per-shard work is the window's ids (64 B per event) plus 1/G of
+// everything else, so the work per GPU falls as G grows:
 //
-//   k_sh_prep    grid   stateless validation (identical on every shard, state_machine.zig:1424-1439,
-//                       1465-1489); for each event that passes, the debit-account owner resolves the
-//                       debit account, the credit-account owner the credit account, the transfer-id
-//                       owner the id (pre-window `exists` comparison, :1506-1507, and in-window
-//                       duplicates through the window key map). Each writes its part of the event's
-//                       9 B of exchange bytes; the other parts stay zero.
-//   (caller)            byte-wise sum all-reduce of the exchange bytes across the shards (RCCL over
-//                       xGMI). Every bit has exactly one writer, so the sum is the union of the parts.
-//   k_sh_decide  grid   every shard now holds the same per-event facts and decides every event the
-//                       same way: account lookups (:1496-1497), ledgers (:1503-1504), exists, then
-//                       linked chains (:1240-1300); identical replies on all shards.
-//   k_sh_count   grid   per-segment failure / owned-insert counts; captures the store base.
-//   k_sh_final   grid   replies, and only owned effects: the id owner appends the record and indexes the
-//                       id, the debit/credit owners add the amount (exact 128-bit atomics).
+//   k_sh_roles    whole window: the ids of each event (64 B); events with a role this shard owns
+//                 (debit account, credit account, transfer id) are compacted, in event order, into
+//                 per-segment lists, so the owned work below runs on dense waves.
+//   k_sh_owned_*  owned events only: read whole and validated (state_machine.zig:1424-1439,
+//                 1465-1489); for those that reach the account checks the owner resolves its side:
+//                 the debit / credit account (ledger, limit flag), or the transfer id (pre-window
+//                 `exists` comparison :1506-1507, in-window duplicates through the window key map).
+//                 Each owner writes its part of the event's 9 B of facts (exchange 1).
+//   k_sh_close    one block: folds the scan blocks' partials (capacity, overflow bound, prefix flag).
+//   (caller)      exchange 1: byte-wise sum all-reduce of the facts (RCCL over xGMI). Every bit has
+//                 exactly one writer, so the sum is the union.
+//   k_sh_home_*   home slice: validation codes and class checks.
+//   k_sh_decide   home slice: account lookups (:1496-1497), ledgers (:1503-1504), exists, then linked
+//                 chains (:1240-1300).
+//   k_sh_count, k_sh_reply   home slice: per-batch replies; one commit bit per event (exchange 2).
+//   (caller)      exchange 2: byte-wise sum all-reduce of the commit bits (E/8 B) and home verdicts.
+//   k_sh_icount, k_sh_apply  whole window, owned roles only: the verdict, then the account owners add
+//                 the amounts (exact 128-bit atomics) and the id owner appends the record.
 //
 // The sharded class is the order-free one: no balance read (no limit flag on a touched
 // account, no balancing), no two-phase, no in-window duplicate id, overflow-free window. Then every
 // event's outcome is a function of the owners' facts alone, and the effects commute. A window outside
-// the class is detected before anything is applied, identically on every shard (its flags travel in
-// the exchange's trailer or follow from the reduced bytes), and fails with TBG_E_UNSUPPORTED at
-// tbg_sync: no shard applies any of it.
+// the class is detected before anything is applied (by an owner: exchange 1's trailer; by a home:
+// exchange 2's trailer), so every shard reaches the same verdict and the window fails with
+// TBG_E_UNSUPPORTED at tbg_sync: no shard applies any of it.
 #pragma once
 #include "sm_logic.h"
 #include "walker.h"
@@ -126,10 +132,19 @@ __device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bo
   g->batch_huge = 0;
 }
 
-// After prep (stream-ordered, one block): folds the prep blocks' partials (amount sums, huge /
-// unsupported bits, owned-id counts; no same-address atomics across blocks) and closes the window's
-// local facts into the trailer words: unsupported, capacity and overflow verdicts. (A separate
-// launch, not a last-block pattern: no device fences in the sharded kernels.)
+// Exchange 2 (commit bits): 16 B trailer (u32 [0]: homes that found an event outside the class),
+// then one bit per event, in 64-bit words (a word may hold bits of two homes: distinct bits).
+__host__ __device__ inline uint64_t xch2_bytes(uint32_t E) { return 16 + 8ull * ((E + 63) / 64); }
+
+// Scan-block partials (Scratch::blk_aux): bit 0 huge amount, bit 1 in-window duplicate id (outside the
+// class), bit 2 ids not strictly increasing (or >= 2^64), bit 3 the window's first id is above every
+// stored id, owned ids reaching the exists check << 4.
+enum : uint32_t { SHX_HUGE = 1, SHX_DUP = 2, SHX_NONMONO = 4, SHX_FRESH = 8, SHX_OWN_SHIFT = 4 };
+
+// After the scan (stream-ordered, one block): folds the scan blocks' partials (no same-address
+// atomics across blocks) into the window's local verdicts: trailer words 0 (duplicate id), 1
+// (capacity), 2 (overflow bound); Globals::win_flags bit 1 (the owned records extend the sorted
+// prefix). (A separate launch, not a last-block pattern: no device fences in the sharded kernels.)
 __global__ void __launch_bounds__(1024) k_sh_close(Dev d, Scratch s, uint32_t nblk, uint32_t* trailer, uint32_t xfer) {
   __shared__ u128 red[1024];
   __shared__ uint32_t bits;
@@ -144,8 +159,8 @@ __global__ void __launch_bounds__(1024) k_sh_close(Dev d, Scratch s, uint32_t nb
   unsigned long long own = 0;
   for (uint32_t j = threadIdx.x; j < nblk; j += 1024) {
     const uint32_t x = s.blk_aux[j];
-    a |= x & 3u;
-    own += x >> 2;
+    a |= x & 15u;
+    own += x >> SHX_OWN_SHIFT;
     if (xfer) v += s.blk_amt[j];
   }
   if (a) atomicOr(&bits, a);
@@ -153,163 +168,252 @@ __global__ void __launch_bounds__(1024) k_sh_close(Dev d, Scratch s, uint32_t nb
   const u128 tot = xfer ? block_sum_u128(v, red) : (u128)0;
   if (threadIdx.x != 0) return;
   Globals* g = d.g;
-  g->sh_own = 0;
-  g->sh_unsup = 0;  // the previous window's verdict (read by every block of its k_sh_final)
-  if (bits & 2u) trailer[0] = 1;
+  if (bits & SHX_DUP) trailer[0] = 1;
   if (xfer) {
     g->batch_amount_sum += tot;
-    if (bits & 1u) g->batch_huge = 1;
+    if (bits & SHX_HUGE) g->batch_huge = 1;
     if (g->x_count + own_s > d.x_max) trailer[1] = 1;
     if (window_ovf_mode(g)) trailer[2] = 1;
+    // every owned balance field stays below 2^64 this window: k_sh_apply's adds need no carry
+    const u128 top = g->ovf_bound + g->batch_amount_sum;
+    g->small_win = (!g->batch_huge && top >= g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1u : 0u;
+    const bool prefix = !(bits & SHX_NONMONO) && (bits & SHX_FRESH) && g->x_sorted == g->x_count;
+    g->win_flags = prefix ? 2u : 0u;
   } else {
     if (g->acc_count + own_s > d.acc_max) trailer[1] = 1;
   }
 }
 
+// Validation a create_transfers event gets on every shard that looks at it whole (its owners and its
+// home): timestamp (:1253-1259), head and field checks (:1465-1489, 1614-1624). Returns the static
+// code or CONT; *reach: the event goes on to the account checks; *unsup: it is valid so far but
+// outside the sharded class (pending, balancing, post/void).
+__device__ inline uint32_t sh_static_ct(tb_transfer_t& t, const WinDesc& w, uint32_t b, uint32_t i, uint32_t* cls,
+                                        bool* reach, bool* unsup) {
+  *reach = false;
+  *unsup = false;
+  const uint16_t f = t.flags;
+  if (f & TB_TRANSFER_LINKED) *cls |= C_LINKED;
+  if (t.timestamp != 0) {
+    *cls |= C_TSNZ;
+    return TB_CT_TIMESTAMP_MUST_BE_ZERO;
+  }
+  t.timestamp = win_ts(w, b, i);
+  uint32_t code = ct_head(t);
+  if (code != CONT) return code;
+  if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
+    code = pv_validate(t);
+    if (code == CONT) *unsup = true;  // two-phase resolution: outside the sharded class
+    return code;
+  }
+  code = ct_validate(t);
+  if (code == CONT) {
+    if (f & (TB_TRANSFER_PENDING | TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT)) *unsup = true;
+    *reach = true;
+  }
+  return code;
+}
+
+__device__ inline uint32_t sh_static_ca(const tb_account_t& a, uint32_t* cls, bool* reach) {
+  *reach = false;
+  if (a.flags & TB_ACCOUNT_LINKED) *cls |= C_LINKED;
+  if (a.timestamp != 0) {
+    *cls |= C_TSNZ;
+    return TB_CA_TIMESTAMP_MUST_BE_ZERO;
+  }
+  const uint32_t code = ca_validate(a);
+  *reach = code == CONT;
+  return code;
+}
+
+// Owned roles of an event (Scratch::bstatus): it reaches the account checks and this shard owns its
+// debit account / credit account / id.
+enum : uint8_t { ROLE_DR = 1, ROLE_CR = 2, ROLE_ID = 4 };
+
 // ------------------------------------------------------------------------------------------------
-// create_transfers: prep
+// scan, in two passes so that the long dependent chains (validation, probes, claims) run on dense
+// waves: k_sh_roles reads the ids of every event and compacts the events with an owned role, in
+// event order, into per-segment lists (Scratch::wlist, segment k at k * SEG, Scratch::cnt_w[k]
+// entries: event | candidate roles << 24); k_sh_owned works through those lists.
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_sh_prep_ct(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
-                                                    uint32_t epoch, XchView xch, uint32_t G, uint32_t me) {
-  __shared__ u128 red[256];
-  __shared__ uint32_t huge_any, unsup, own;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (threadIdx.x == 0) huge_any = unsup = own = 0;
-  if (i == 0) check_window(w, d.g);
+__device__ inline uint32_t ol_event(uint32_t x) { return x & 0xFFFFFFu; }
+__device__ inline uint32_t ol_roles(uint32_t x) { return x >> 24; }
+
+template <bool XFER>
+__global__ void __launch_bounds__(SEG) k_sh_roles(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes, uint32_t E,
+                                                  XchView xch, uint32_t G, uint32_t me) {
+  __shared__ uint32_t lds[SEG / 64];
+  __shared__ uint32_t aux;
+  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
+  if (threadIdx.x == 0) aux = 0;
+  __syncthreads();
+  uint32_t roles = 0;
+  if (i < E) {
+    const uint4* q = reinterpret_cast<const uint4*>(ev_bytes + (size_t)i * 128);
+    const tb_uint128_t id = rw_u128(q[0]);
+    if (shard_of(id.lo, id.hi, G) == me) roles |= ROLE_ID;
+    if (XFER) {
+      const tb_uint128_t dra = rw_u128(q[1]), cra = rw_u128(q[2]);
+      if (shard_of(dra.lo, dra.hi, G) == me) roles |= ROLE_DR;
+      if (shard_of(cra.lo, cra.hi, G) == me) roles |= ROLE_CR;
+      // the owned records extend the sorted prefix if the window's ids are strictly increasing
+      bool nm = id.hi != 0;
+      if (i > 0) nm |= !(id.lo > reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i - 1].id.lo);
+      if (nm) atomicOr(&aux, (uint32_t)SHX_NONMONO);
+      if (i == 0 && id.hi == 0 && id.lo > d.g->x_id_max) atomicOr(&aux, (uint32_t)SHX_FRESH);
+      xch.drl[i] = 0;  // k_sh_owned writes the owned facts
+      xch.crl[i] = 0;
+    }
+    xch.zw[i] = 0;
+  }
+  uint32_t tot;
+  const uint32_t r = block_excl<SEG / 64>(roles ? 1u : 0u, lds, &tot);
+  if (roles) s.wlist[blockIdx.x * SEG + r] = i | (roles << 24);
+  if (threadIdx.x == 0) {
+    s.cnt_w[blockIdx.x] = tot;
+    s.blk_aux[blockIdx.x] = aux;
+  }
+}
+
+// Owned work of segment blockIdx.x: validation, the owned probes / claim / exists, the owner facts.
+// Rewrites each entry's roles to the validated ones (0 unless the event reaches the account checks).
+__global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
+                                                     uint32_t epoch, XchView xch) {
+  __shared__ u128 red[SEG / 64];
+  __shared__ uint32_t aux;
+  const uint32_t k = blockIdx.x * SEG + threadIdx.x;
+  if (threadIdx.x == 0) aux = 0;
+  if (k == 0) check_window(w, d.g);
   __syncthreads();
   u128 amount_upper = 0;
-  if (i < w.E) {
+  const uint32_t n = s.cnt_w[blockIdx.x];
+  if (threadIdx.x < n) {
+    const uint32_t x = s.wlist[k];
+    const uint32_t i = ol_event(x), cand = ol_roles(x);
     tb_transfer_t t = ev[i];
-    const uint32_t b = win_batch(w, i);
-    uint32_t cls = 0, code, dr_slot = NONE32, cr_slot = NONE32, id_ent = NONE32;
-    uint32_t drl = 0, crl = 0, zw = 0;
-    const uint16_t f = t.flags;
-    if (f & TB_TRANSFER_LINKED) cls |= C_LINKED;
-    if (t.timestamp != 0) {
-      cls |= C_TSNZ;
-      code = TB_CT_TIMESTAMP_MUST_BE_ZERO;
-    } else {
-      t.timestamp = win_ts(w, b, i);
-      code = ct_head(t);
-      if (code == CONT && (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))) {
-        code = pv_validate(t);
-        if (code == CONT) atomicOr(&unsup, 1u);  // two-phase resolution: outside the sharded class
-      } else if (code == CONT) {
-        code = ct_validate(t);
-        if (code == CONT) {
-          if (f & (TB_TRANSFER_PENDING | TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT))
-            atomicOr(&unsup, 1u);
-          cls |= C_REACH;
-          amount_upper = U(t.amount);
-          // up to three independent probes, one per owned side
-          if (shard_of(t.debit_account_id.lo, t.debit_account_id.hi, G) == me) {
-            AccEntry e;
-            dr_slot = acc_find(d.acc_tab, d.acc_mask, t.debit_account_id, &e);
-            if (dr_slot != NONE32) {
-              drl = e.ledger;
-              if (e.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) zw |= SH_DR_LIMIT;
-            }
-          }
-          if (shard_of(t.credit_account_id.lo, t.credit_account_id.hi, G) == me) {
-            AccEntry e;
-            cr_slot = acc_find(d.acc_tab, d.acc_mask, t.credit_account_id, &e);
-            if (cr_slot != NONE32) {
-              crl = e.ledger;
-              if (e.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) zw |= SH_CR_LIMIT;
-            }
-          }
-          if (shard_of(t.id.lo, t.id.hi, G) == me) {
-            cls |= C_OWN;
-            atomicAdd(&own, 1u);
-            bool dup;
-            id_ent = sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
-            if (dup) atomicOr(&unsup, 1u);
-            uint32_t xs = NONE32;
-            if (x_may_exist(t.id, d.g->x_id_max)) {
-              xs = x_find(d.x_tab, d.xr, d.x_mask, t.id);
-              if (xs == NONE32) xs = x_prefix_find(d.xr, d.g->x_sorted, t.id);
-            }
-            zw |= 1 + (xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]));
-          }
+    uint32_t cls = 0, roles = 0, drl = 0, crl = 0, zw = 0;
+    bool reach, unsup;
+    (void)sh_static_ct(t, w, win_batch(w, i), i, &cls, &reach, &unsup);
+    if (reach) {
+      roles = cand;
+      if (cand & (ROLE_DR | ROLE_CR)) amount_upper = U(t.amount);
+      // up to three independent probes, one per owned side
+      if (cand & ROLE_DR) {
+        AccEntry e;
+        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, t.debit_account_id, &e);
+        s.dr_slot[i] = slot;
+        if (slot != NONE32) {
+          drl = e.ledger;
+          if (e.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) zw |= SH_DR_LIMIT;
         }
+        xch.drl[i] = drl;
       }
+      if (cand & ROLE_CR) {
+        AccEntry e;
+        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, t.credit_account_id, &e);
+        s.cr_slot[i] = slot;
+        if (slot != NONE32) {
+          crl = e.ledger;
+          if (e.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) zw |= SH_CR_LIMIT;
+        }
+        xch.crl[i] = crl;
+      }
+      if (cand & ROLE_ID) {
+        atomicAdd(&aux, 1u << SHX_OWN_SHIFT);
+        bool dup;
+        (void)sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
+        if (dup) atomicOr(&aux, (uint32_t)SHX_DUP);
+        uint32_t xs = NONE32;
+        if (x_may_exist(t.id, d.g->x_id_max)) {
+          xs = x_find(d.x_tab, d.xr, d.x_mask, t.id);
+          if (xs == NONE32) xs = x_prefix_find(d.xr, d.g->x_sorted, t.id);
+        }
+        zw |= 1 + (xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]));
+      }
+      xch.zw[i] = (uint8_t)zw;
     }
-    if (code != CONT) cls |= C_STATIC;
-    s.code[i] = code;
-    s.cls[i] = cls;
-    s.batch[i] = (uint16_t)b;
-    s.dr_slot[i] = dr_slot;
-    s.cr_slot[i] = cr_slot;
-    s.id_ent[i] = id_ent;
-    xch.drl[i] = drl;
-    xch.crl[i] = crl;
-    xch.zw[i] = (uint8_t)zw;
+    s.wlist[k] = i | (roles << 24);
   }
-  if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&huge_any, 1u);
-  red[threadIdx.x] = ((uint64_t)(amount_upper >> 64) != 0) ? 0 : amount_upper;
+  if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&aux, (uint32_t)SHX_HUGE);
+  // block sum of the amounts below 2^64: wave sums of the two 64-bit halves, then one LDS word per wave
+  const uint64_t a = ((uint64_t)(amount_upper >> 64) != 0) ? 0ull : (uint64_t)amount_upper;
+  u128 v = a;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t lo = __shfl_xor((unsigned long long)(uint64_t)v, o, 64);
+    const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(v >> 64), o, 64);
+    v += ((u128)hi << 64) | lo;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {  // this block's partials (k_sh_close folds them)
-    s.blk_amt[blockIdx.x] = red[0];
-    s.blk_aux[blockIdx.x] = (huge_any ? 1u : 0u) | (unsup ? 2u : 0u) | (own << 2);
+  if (threadIdx.x == 0) {  // this segment's partials (k_sh_close folds them)
+    u128 tot = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < SEG / 64; w2++) tot += red[w2];
+    s.blk_amt[blockIdx.x] = tot;
+    s.blk_aux[blockIdx.x] |= aux;  // k_sh_roles wrote the segment's prefix bits
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// create_accounts: prep
-// ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_sh_prep_ca(Dev d, Scratch s, const tb_account_t* __restrict__ ev, WinDesc w,
-                                                    uint32_t epoch, XchView xch, uint32_t G, uint32_t me) {
-  __shared__ uint32_t unsup, own;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (threadIdx.x == 0) unsup = own = 0;
-  if (i == 0) check_window(w, d.g);
+__global__ void __launch_bounds__(SEG) k_sh_owned_ca(Dev d, Scratch s, const tb_account_t* __restrict__ ev, WinDesc w,
+                                                     uint32_t epoch, XchView xch) {
+  __shared__ uint32_t aux;
+  const uint32_t k = blockIdx.x * SEG + threadIdx.x;
+  if (threadIdx.x == 0) aux = 0;
+  if (k == 0) check_window(w, d.g);
   __syncthreads();
-  if (i < w.E) {
+  const uint32_t n = s.cnt_w[blockIdx.x];
+  if (threadIdx.x < n) {
+    const uint32_t i = ol_event(s.wlist[k]);
     const tb_account_t a = ev[i];
-    const uint32_t b = win_batch(w, i);
-    uint32_t cls = 0, code, id_ent = NONE32, zw = 0;
-    if (a.flags & TB_ACCOUNT_LINKED) cls |= C_LINKED;
-    if (a.timestamp != 0) {
-      cls |= C_TSNZ;
-      code = TB_CA_TIMESTAMP_MUST_BE_ZERO;
-    } else {
-      code = ca_validate(a);
-      if (code == CONT) {
-        cls |= C_REACH;
-        if (shard_of(a.id.lo, a.id.hi, G) == me) {
-          cls |= C_OWN;
-          atomicAdd(&own, 1u);
-          bool dup;
-          id_ent = sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), a.id, i, w.E, epoch, &dup);
-          if (dup) atomicOr(&unsup, 1u);
-          AccEntry e;
-          const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, a.id, &e);
-          zw = 1 + (slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(a, d.acc[slot]));
-        }
-      }
+    uint32_t cls = 0, roles = 0;
+    bool reach;
+    (void)sh_static_ca(a, &cls, &reach);
+    if (reach) {
+      roles = ROLE_ID;
+      atomicAdd(&aux, 1u << SHX_OWN_SHIFT);
+      bool dup;
+      (void)sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), a.id, i, w.E, epoch, &dup);
+      if (dup) atomicOr(&aux, (uint32_t)SHX_DUP);
+      AccEntry e;
+      const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, a.id, &e);
+      xch.zw[i] = (uint8_t)(1 + (slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(a, d.acc[slot])));
     }
-    if (code != CONT) cls |= C_STATIC;
-    s.code[i] = code;
-    s.cls[i] = cls;
-    s.batch[i] = (uint16_t)b;
-    s.id_ent[i] = id_ent;
-    s.dr_slot[i] = NONE32;
-    s.cr_slot[i] = NONE32;
-    xch.zw[i] = (uint8_t)zw;
+    s.wlist[k] = i | (roles << 24);
   }
   __syncthreads();
-  if (threadIdx.x == 0) s.blk_aux[blockIdx.x] = (unsup ? 2u : 0u) | (own << 2);  // k_sh_close folds them
+  if (threadIdx.x == 0) s.blk_aux[blockIdx.x] |= aux;
 }
 
 // ------------------------------------------------------------------------------------------------
-// decide: every shard, every event, from the reduced exchange words.
+// home slice [e0, e1): validation codes, decisions, replies, commit bits.
 // ------------------------------------------------------------------------------------------------
 template <bool XFER>
-__device__ inline uint32_t sh_code(const Dev& d, const Scratch& s, const uint8_t* ev, const XchView& xch, uint32_t j) {
+__global__ void __launch_bounds__(256) k_sh_home(Scratch s, const uint8_t* __restrict__ ev_bytes, WinDesc w,
+                                                 uint32_t e0, uint32_t e1, uint32_t* trailer2) {
+  const uint32_t i = e0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= e1) return;
+  const uint32_t b = win_batch(w, i);
+  uint32_t cls = 0, code;
+  bool reach, unsup = false;
+  if (XFER) {
+    tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
+    code = sh_static_ct(t, w, b, i, &cls, &reach, &unsup);
+  } else {
+    code = sh_static_ca(reinterpret_cast<const tb_account_t*>(ev_bytes)[i], &cls, &reach);
+  }
+  if (unsup) atomicOr(&trailer2[0], 1u);
+  if (reach) cls |= C_REACH;
+  if (code != CONT) cls |= C_STATIC;
+  s.code[i] = code;
+  s.cls[i] = cls;
+  s.batch[i] = (uint16_t)b;
+}
+
+// An event's code from the exchanged owner facts (its static code first).
+template <bool XFER>
+__device__ inline uint32_t sh_code(const Scratch& s, const uint8_t* ev, const XchView& xch, uint32_t j,
+                                   uint32_t* trailer2) {
   const uint32_t code = s.code[j];
   if (code != CONT) return code;
   const uint32_t zw = xch.zw[j];
@@ -324,23 +428,23 @@ __device__ inline uint32_t sh_code(const Dev& d, const Scratch& s, const uint8_t
   if (z != TB_CT_OK) return z;  // exists* (:1506-1507)
   // Reaches the balance checks: overflow cannot fail in a class window; a limit flag on either
   // account is a balance read (:1546-1547), outside the class.
-  if (zw & (SH_DR_LIMIT | SH_CR_LIMIT)) atomicOr(&d.g->sh_unsup, 1u);
+  if (zw & (SH_DR_LIMIT | SH_CR_LIMIT)) atomicOr(&trailer2[0], 1u);
   return TB_CT_OK;
 }
 
 template <bool XFER>
-__global__ void __launch_bounds__(256) k_sh_decide(Dev d, Scratch s, const uint8_t* ev, WinDesc w, XchView xch) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0 && (xch.trailer[0] | xch.trailer[1] | xch.trailer[2])) atomicOr(&d.g->sh_unsup, 1u);
-  if (i >= w.E) return;
+__global__ void __launch_bounds__(256) k_sh_decide(Scratch s, const uint8_t* ev, WinDesc w, uint32_t e0, uint32_t e1,
+                                                   XchView xch, uint32_t* trailer2) {
+  const uint32_t i = e0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= e1) return;
   const uint32_t b = s.batch[i];
   const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
   if (i != first && (s.cls[i - 1] & C_LINKED)) return;  // chain member: its head decides
   const uint32_t cls = s.cls[i];
   if (!(cls & C_LINKED)) {
-    const uint32_t code = sh_code<XFER>(d, s, ev, xch, i);
+    const uint32_t code = sh_code<XFER>(s, ev, xch, i, trailer2);
     s.code[i] = code;
-    if (code == TB_CT_OK) s.cls[i] = cls | C_COMMIT | ((cls & C_OWN) ? C_INSERTED : 0u);
+    if (code == TB_CT_OK) s.cls[i] = cls | C_COMMIT;
     return;
   }
   // chain head: members i..end (:1240-1300). No member's outcome depends on another member's
@@ -348,7 +452,7 @@ __global__ void __launch_bounds__(256) k_sh_decide(Dev d, Scratch s, const uint8
   uint32_t end = i, f = NONE32;
   for (uint32_t j = i;; j++) {
     const bool lj = s.cls[j] & C_LINKED;
-    uint32_t code = sh_code<XFER>(d, s, ev, xch, j);
+    uint32_t code = sh_code<XFER>(s, ev, xch, j, trailer2);
     if (lj && j == last) code = TB_CT_LINKED_EVENT_CHAIN_OPEN;  // :1247
     s.code[j] = code;
     if (code != TB_CT_OK && f == NONE32) f = j;
@@ -358,112 +462,151 @@ __global__ void __launch_bounds__(256) k_sh_decide(Dev d, Scratch s, const uint8
   for (uint32_t j = i; j <= end; j++) {
     const uint32_t cj = s.cls[j];
     if (f == NONE32) {
-      s.cls[j] = cj | C_COMMIT | ((cj & C_OWN) ? C_INSERTED : 0u);
+      s.cls[j] = cj | C_COMMIT;
     } else if (j != f && !((cj & C_LINKED) && j == last)) {
       s.code[j] = TB_CT_LINKED_EVENT_FAILED;  // back-fill before f, broken chain after f
     }
   }
 }
 
-// Per-segment failure / owned-insert counts (k_wcount with the sharded boundary fences).
-__global__ void __launch_bounds__(SEG) k_sh_count(Dev d, Scratch s, uint32_t E, uint32_t xfer) {
+// Home slice, per segment k0 + blockIdx.x (segments are window-aligned, SEG events): failure counts.
+__global__ void __launch_bounds__(SEG) k_sh_count(Scratch s, uint32_t e0, uint32_t e1, uint32_t k0) {
   __shared__ uint32_t lds[SEG / 64];
-  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
-  if (i == 0) d.g->base = xfer ? d.g->x_count : d.g->acc_count;  // k_sh_final's store base
-  uint32_t nbad = 0, nins = 0;
-  if (i < E) {
-    nbad = s.code[i] != TB_CT_OK;
-    nins = (s.cls[i] & C_INSERTED) ? 1u : 0u;
-  }
-  nbad = block_sum<SEG / 64>(nbad, lds);
-  nins = block_sum<SEG / 64>(nins, lds);
-  if (threadIdx.x == 0) {
-    s.cnt_bad[blockIdx.x] = nbad;
-    s.cnt_ins[blockIdx.x] = nins;
-  }
+  const uint32_t i = (k0 + blockIdx.x) * SEG + threadIdx.x;
+  const uint32_t nbad = (i >= e0 && i < e1 && s.code[i] != TB_CT_OK) ? 1u : 0u;
+  const uint32_t tot = block_sum<SEG / 64>(nbad, lds);
+  if (threadIdx.x == 0) s.cnt_bad[blockIdx.x] = tot;
 }
 
-// ------------------------------------------------------------------------------------------------
-// final: replies (every shard) and owned effects.
-// ------------------------------------------------------------------------------------------------
-template <bool XFER>
-__global__ void __launch_bounds__(SEG) k_sh_final(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w, FinalOut o) {
+// Home slice: replies of batches [hb0, hb1) (batch_base relative to hb0, indices batch-relative) and
+// the commit bit of every slice event (one 64-bit word per wave; words are window-aligned).
+__global__ void __launch_bounds__(SEG) k_sh_reply(Dev d, Scratch s, WinDesc w, uint32_t hb0, uint32_t hb1, uint32_t e0,
+                                                  uint32_t e1, uint32_t k0, FinalOut o, unsigned long long* bits) {
   __shared__ uint32_t lds[SEG / 64];
-  __shared__ unsigned long long ldsm[SEG / 64];
-  Globals* g = d.g;
-  const bool unsup = __hip_atomic_load(&g->sh_unsup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  const uint32_t E = w.E;
-  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
+  const uint32_t i = (k0 + blockIdx.x) * SEG + threadIdx.x;
+  const bool mine = i >= e0 && i < e1;
   uint32_t cls = 0, code = TB_CT_OK;
-  if (i < E) {
+  if (mine) {
     cls = s.cls[i];
     code = s.code[i];
   }
-  bool ins = (cls & C_INSERTED) != 0;
   const uint32_t bad = code != TB_CT_OK;
   const uint32_t pbad = seg_prefix<SEG>(s.cnt_bad, blockIdx.x, lds);
-  const uint32_t pins = seg_prefix<SEG>(s.cnt_ins, blockIdx.x, lds);
-  uint32_t tot_bad, tot_ins;
+  uint32_t tot_bad;
   const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
-  const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
-  if (XFER) {
-    const unsigned long long key =
-        (!unsup && ins && i < E) ? x_id_key(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].id) : 0ull;
-    const unsigned long long m = block_max_u64<SEG / 64>(key, ldsm);
-    if (threadIdx.x == 0 && m > g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&g->x_id_max), m);
-  }
-  if (i >= E) return;
-  if (unsup) {
-    if (i == 0) atomicOr(&g->window_error, 2u);
-    if (i == E - 1) sh_window_reset(g, XFER, 0, false);
-    return;
-  }
-  const uint64_t xbase = g->base;  // captured by k_sh_count: the last thread rewrites the count
+  const unsigned long long m = __ballot(mine && (cls & C_COMMIT));
+  if ((threadIdx.x & 63) == 0 && i < e1 && i + 64 > e0) bits[i / 64] = m;
+  if (!mine) return;
   const uint32_t b = s.batch[i];
   if (i == w.off[b]) {
-    for (int32_t bb = (int32_t)b; bb >= 0 && w.off[bb] == i; bb--) o.batch_base[bb] = rbad;
+    // event i opens batch b and every empty home batch just before it
+    for (int32_t bb = (int32_t)b; bb >= (int32_t)hb0 && w.off[bb] == i; bb--) o.batch_base[bb - hb0] = rbad;
   }
-  if (bad && sh_guard(g, rbad < E, 2, rbad)) {
+  if (bad && sh_guard(d.g, rbad < e1 - e0, 2, rbad)) {
     tb_create_result_t r;
     r.index = i - w.off[b];
     r.result = code;
     o.results[rbad] = r;
   }
+  if (i == e1 - 1) {
+    const uint32_t total_bad = rbad + bad;
+    for (int32_t bb = (int32_t)hb1; bb >= (int32_t)hb0 && w.off[bb] == e1; bb--) o.batch_base[bb - hb0] = total_bad;
+    if (o.out_count) *o.out_count = total_bad;
+    d.g->result_count = total_bad;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// apply: whole window, owned roles of committed events.
+// ------------------------------------------------------------------------------------------------
+__device__ inline bool sh_bit(const unsigned long long* bits, uint32_t i) { return (bits[i / 64] >> (i & 63)) & 1ull; }
+
+// Verdict of the window, identical on every shard: exchange 1's trailer (owners: duplicate id,
+// capacity, overflow bound) or exchange 2's (homes: an event outside the class).
+__device__ inline bool sh_abort(const uint32_t* trailer1, const uint32_t* trailer2) {
+  return (trailer1[0] | trailer1[1] | trailer1[2] | trailer2[0]) != 0;
+}
+
+// Per segment: committed owned-id entries (insert counts), over the segment lists.
+__global__ void __launch_bounds__(SEG) k_sh_icount(Dev d, Scratch s, uint32_t xfer, const unsigned long long* bits) {
+  __shared__ uint32_t lds[SEG / 64];
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.g->base = xfer ? d.g->x_count : d.g->acc_count;  // k_sh_apply's base
+  uint32_t ins = 0;
+  if (threadIdx.x < s.cnt_w[blockIdx.x]) {
+    const uint32_t x = s.wlist[blockIdx.x * SEG + threadIdx.x];
+    ins = ((ol_roles(x) & ROLE_ID) && sh_bit(bits, ol_event(x))) ? 1u : 0u;
+  }
+  const uint32_t tot = block_sum<SEG / 64>(ins, lds);
+  if (threadIdx.x == 0) s.cnt_ins[blockIdx.x] = tot;
+}
+
+template <bool XFER>
+__global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w,
+                                                  const uint32_t* trailer1, const uint32_t* trailer2,
+                                                  const unsigned long long* bits) {
+  __shared__ uint32_t lds[SEG / 64];
+  __shared__ unsigned long long ldsm[SEG / 64];
+  Globals* g = d.g;
+  const bool last_block = blockIdx.x == gridDim.x - 1;
+  if (sh_abort(trailer1, trailer2)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&g->window_error, 2u);
+    if (last_block && threadIdx.x == 0) sh_window_reset(g, XFER, 0, false);
+    return;
+  }
+  const bool prefix_win = XFER && (g->win_flags & 2u) != 0;  // k_sh_close
+  const bool small = XFER && g->small_win != 0;              // k_sh_close
+  const uint64_t xbase = g->base;  // captured by k_sh_icount: the last block rewrites the count
+  const uint32_t n = s.cnt_w[blockIdx.x];
+  uint32_t i = 0, roles = 0;
+  bool commit = false;
+  if (threadIdx.x < n) {
+    const uint32_t x = s.wlist[blockIdx.x * SEG + threadIdx.x];
+    i = ol_event(x);
+    roles = ol_roles(x);
+    commit = roles && sh_bit(bits, i);
+  }
+  bool ins = commit && (roles & ROLE_ID);
+  const uint32_t pins = seg_prefix<SEG>(s.cnt_ins, blockIdx.x, lds);
+  uint32_t tot_ins;
+  const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
   if (XFER) {
-    uint32_t drs = s.dr_slot[i], crs = s.cr_slot[i];
-    if (drs != NONE32 && !sh_guard(g, drs < d.acc_max, 3, drs)) drs = NONE32;
-    if (crs != NONE32 && !sh_guard(g, crs < d.acc_max, 4, crs)) crs = NONE32;
-    if (ins && !sh_guard(g, xbase + rins < d.x_max, 5, xbase + rins)) ins = false;
-    if ((cls & C_COMMIT) && ((drs != NONE32) | (crs != NONE32) | ins)) {
+    const unsigned long long key = ins ? x_id_key(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].id) : 0ull;
+    const unsigned long long m = block_max_u64<SEG / 64>(key, ldsm);
+    if (threadIdx.x == 0 && m > g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&g->x_id_max), m);
+  }
+  if (commit) {
+    if (XFER) {
+      uint32_t drs = (roles & ROLE_DR) ? s.dr_slot[i] : NONE32, crs = (roles & ROLE_CR) ? s.cr_slot[i] : NONE32;
+      if (drs != NONE32 && !sh_guard(g, drs < d.acc_max, 3, drs)) drs = NONE32;
+      if (crs != NONE32 && !sh_guard(g, crs < d.acc_max, 4, crs)) crs = NONE32;
+      if (ins && !sh_guard(g, xbase + rins < d.x_max, 5, xbase + rins)) ins = false;
       tb_transfer_t t2 = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
       const u128 a = U(t2.amount);
       Add128 a_dr, a_cr;
-      if (drs != NONE32) a_dr.issue(&d.acc[drs].debits_posted, a, false);
-      if (crs != NONE32) a_cr.issue(&d.acc[crs].credits_posted, a, false);
+      if (drs != NONE32) a_dr.issue(&d.acc[drs].debits_posted, a, small);
+      if (crs != NONE32) a_cr.issue(&d.acc[crs].credits_posted, a, small);
       if (ins) {
         const uint64_t slot = xbase + rins;
-        t2.timestamp = win_ts(w, b, i);
+        t2.timestamp = win_ts(w, win_batch(w, i), i);
         d.xr[slot] = t2;
-        x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
+        if (!prefix_win) x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
         d.xstatus[slot] = 0;
       }
       a_dr.finish();
       a_cr.finish();
+    } else if (ins && sh_guard(g, xbase + rins < d.acc_max, 6, xbase + rins)) {
+      const uint64_t slot = xbase + rins;
+      tb_account_t a = reinterpret_cast<const tb_account_t*>(ev_bytes)[i];
+      a.timestamp = win_ts(w, win_batch(w, i), i);
+      d.acc[slot] = a;
+      d.hot[slot] = 0;
+      acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
     }
-  } else if (ins && sh_guard(g, xbase + rins < d.acc_max, 6, xbase + rins)) {
-    const uint64_t slot = xbase + rins;
-    tb_account_t a = reinterpret_cast<const tb_account_t*>(ev_bytes)[i];
-    a.timestamp = win_ts(w, b, i);
-    d.acc[slot] = a;
-    d.hot[slot] = 0;
-    acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
   }
-  if (i == E - 1) {
-    const uint32_t total_bad = rbad + bad, total_ins = rins + (ins ? 1u : 0u);
-    for (int32_t bb = (int32_t)w.nb; bb >= 0 && w.off[bb] == E; bb--) o.batch_base[bb] = total_bad;
-    if (o.out_count) *o.out_count = total_bad;
-    g->result_count = total_bad;
-    g->events_total += E;
-    sh_window_reset(g, XFER, xbase + total_ins, true);
+  if (last_block && threadIdx.x == 0) {
+    const uint64_t total = xbase + pins + tot_ins;
+    g->events_total += w.E;
+    if (prefix_win) g->x_sorted = total;
+    sh_window_reset(g, XFER, total, true);
   }
 }

@@ -2,15 +2,21 @@
 
 Account a lives on shard `shard_of(a.id)`, transfer t on shard `shard_of(t.id)` (csrc/shard.h).
 Every shard receives the same prepared window (the replica hands each GPU the same prepare body,
-state_machine.zig:1107-1146) and commits it in three steps through the C ABI (include/tbg.h):
+state_machine.zig:1107-1146) and is the home of a contiguous range of its batches (`home_range`).
+A window commits in five steps through the C ABI (include/tbg.h):
 
-  tbg_shard_prepare_window   validate; resolve the owned accounts / ids; write exchange words
-  exchange                   byte-wise sum of the exchange bytes across the shards (9 B per transfer:
-                             debit / credit ledger, exists code + limit bits; one writer per bit), on
-                             the engine's stream (RCCL uint8 all-reduce over xGMI: torch "nccl")
-  tbg_shard_commit_window    decide every event (identically on every shard); owned effects only
+  tbg_shard_prepare_window   owned roles only: validate, resolve the owned accounts / ids, write the
+                             owner facts (9 B per transfer: debit / credit ledger, exists code +
+                             limit bits; one writer per bit)
+  exchange                   byte-wise sum of the facts across the shards, on the engine's stream
+                             (RCCL uint8 all-reduce over xGMI: torch "nccl")
+  tbg_shard_decide_window    home batches only: decide, write their replies and one commit bit per
+                             event
+  exchange                   byte-wise sum of the commit bits (E/8 B) across the shards
+  tbg_shard_commit_window    owned effects of the committed events
 
 The `exchange` callable is the only collective on the data path; with one shard there is none.
+Per shard, the work is the window's ids plus 1/G of the rest: it falls as G grows.
 """
 import ctypes
 
@@ -61,6 +67,13 @@ def exchange_gloo(t):
     torch.cuda.current_stream().synchronize()
 
 
+def home_range(n_batches, shard_count, shard_index):
+    """Home batches [first, first + count) of `shard_index`: contiguous, as even as possible."""
+    lo = n_batches * shard_index // shard_count
+    hi = n_batches * (shard_index + 1) // shard_count
+    return lo, hi - lo
+
+
 class ShardedStateMachine:
     """One shard of a hash-sharded engine. `exchange(t)` must sum the uint8 tensor `t` in place
     across all shards (None for a single shard)."""
@@ -75,8 +88,11 @@ class ShardedStateMachine:
         self.shard_count, self.shard_index = shard_count, shard_index
         self.exchange = exchange
         events_max = window_events_max or batch_max
-        self.xch = torch.zeros(16 + 9 * events_max, dtype=torch.uint8, device=torch.device("cuda", device))
-        self.stream = torch.cuda.ExternalStream(self.sm.stream, device=torch.device("cuda", device))
+        dev = torch.device("cuda", device)
+        self.xch = torch.zeros(16 + 9 * events_max, dtype=torch.uint8, device=dev)
+        self.bits = torch.zeros(int(_lib.lib().tbg_shard_commit_bits_bytes(events_max)), dtype=torch.uint8, device=dev)
+        self.stream = torch.cuda.ExternalStream(self.sm.stream, device=dev)
+        self._n_events = 0
         torch.cuda.synchronize(device)
 
     @property
@@ -86,29 +102,48 @@ class ShardedStateMachine:
     def close(self):
         self.sm.close()
 
+    def home_range(self, n_batches):
+        return home_range(n_batches, self.shard_count, self.shard_index)
+
     def prepare_window(self, operation, d_events, batch_events, batch_timestamps):
+        """Step 1; returns the facts tensor to be summed across the shards."""
         nb = len(batch_events)
         ev = (ctypes.c_uint32 * nb)(*batch_events)
         ts = (ctypes.c_uint64 * nb)(*batch_timestamps)
         _lib.check(_lib.lib().tbg_shard_prepare_window(self.sm.h, int(operation), d_events, nb, ev, ts,
                                                        self.xch.data_ptr()), "shard_prepare_window")
-        n = _lib.lib().tbg_shard_exchange_bytes(int(operation), sum(batch_events))
+        self._n_events = sum(batch_events)
+        n = _lib.lib().tbg_shard_exchange_bytes(int(operation), self._n_events)
         return self.xch[:n]
 
-    def commit_prepared(self, d_results, d_batch_base):
-        _lib.check(_lib.lib().tbg_shard_commit_window(self.sm.h, self.xch.data_ptr(), d_results, d_batch_base),
+    def decide_window(self, home_first, home_count, d_results, d_batch_base):
+        """Step 3 (after the facts were summed); returns the commit-bit tensor to be summed."""
+        _lib.check(_lib.lib().tbg_shard_decide_window(self.sm.h, self.xch.data_ptr(), home_first, home_count,
+                                                      d_results, d_batch_base, self.bits.data_ptr()),
+                   "shard_decide_window")
+        return self.bits[:_lib.lib().tbg_shard_commit_bits_bytes(self._n_events)]
+
+    def commit_decided(self):
+        """Step 5 (after the commit bits were summed)."""
+        _lib.check(_lib.lib().tbg_shard_commit_window(self.sm.h, self.xch.data_ptr(), self.bits.data_ptr()),
                    "shard_commit_window")
 
     def commit_window(self, operation, d_events, batch_events, batch_timestamps, d_results, d_batch_base):
-        """Asynchronous on the engine stream; results land in d_results / d_batch_base exactly as
-        tbg_commit_window's (identical on every shard)."""
+        """Asynchronous on the engine stream. Replies of this shard's home batches (home_range) land
+        in d_results / d_batch_base (d_batch_base[0..home_count]); returns (home_first, home_count)."""
         import torch
 
+        first, count = self.home_range(len(batch_events))
         words = self.prepare_window(operation, d_events, batch_events, batch_timestamps)
         if self.exchange is not None:
             with torch.cuda.stream(self.stream):
                 self.exchange(words)
-        self.commit_prepared(d_results, d_batch_base)
+        bits = self.decide_window(first, count, d_results, d_batch_base)
+        if self.exchange is not None:
+            with torch.cuda.stream(self.stream):
+                self.exchange(bits)
+        self.commit_decided()
+        return first, count
 
     def sync(self):
         self.sm.sync()

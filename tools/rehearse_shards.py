@@ -1,13 +1,14 @@
 """Per-shard GPU time of the hash-sharded commit at G shards, rehearsed on ONE GPU.
 
 G ShardedStateMachine engines live on cuda:0 in this process. Each window runs shard by shard
-(prepare -> in-process byte-wise sum of the exchange bytes, i.e. what the RCCL all-reduce computes
--> commit), with HIP events on each engine's stream around its prepare and commit. A shard's GPU
-time per window is what one GPU of a G-GPU node spends on the window apart from the collective, so
+(prepare -> in-process byte-wise sum of the facts, i.e. what the RCCL all-reduce computes -> decide
+(home batches) -> sum of the commit bits -> commit), with HIP events on each engine's stream around
+each step. A shard's GPU time per window is what one GPU of a G-GPU node spends on the window apart
+from the collectives, so
 
-    estimated G-GPU rate = global events / sum over windows of max over shards (prep + commit)
+    estimated G-GPU rate = global events / sum over windows of max over shards (prep + decide + commit)
 
-is an upper bound for the real node (the all-reduce of the window's 9 B/event is added on top).
+is an upper bound for the real node (the all-reduces of 9 B + 1 bit per event are added on top).
 Not a bench line: evidence for DESIGN.md §7. Usage (on the GPU box):
 
     python tools/rehearse_shards.py --shards 8 --accounts 2000000 --transfers 40000000 --window 64
@@ -57,6 +58,27 @@ def main():
     prepare_ts = 0
     times = []  # per window: per shard (prep ms, commit ms)
 
+    def timed_step(fn):
+        """Runs fn() on each shard's stream between two events; returns fn's results and the events."""
+        outs, evs = [], []
+        for r, s in enumerate(shards):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(s.stream):
+                e0.record()
+                outs.append(fn(r, s))
+                e1.record()
+            s.stream.synchronize()
+            evs.append((e0, e1))
+        return outs, evs
+
+    def summed(tensors):
+        total = tensors[0].clone()
+        for t in tensors[1:]:
+            total += t
+        for t in tensors:
+            t.copy_(total)
+        torch.cuda.synchronize()
+
     def window(op, d_ev, b0, b1, n_total, timed):
         nonlocal prepare_ts
         ns, ts = [], []
@@ -66,33 +88,17 @@ def main():
             ns.append(n)
             ts.append(prepare_ts)
         ptr = d_ev.data_ptr() + b0 * BATCH * 128
-        words, evs = [], []
-        for s in shards:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            with torch.cuda.stream(s.stream):
-                e0.record()
-                words.append(s.prepare_window(op, ptr, ns, ts))
-                e1.record()
-            s.stream.synchronize()
-            evs.append([e0, e1])
-        total = words[0].clone()
-        for w in words[1:]:
-            total += w
-        for w in words:
-            w.copy_(total)
-        torch.cuda.synchronize()
-        for r, s in enumerate(shards):
-            e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            with torch.cuda.stream(s.stream):
-                e2.record()
-                s.commit_prepared(d_res.data_ptr(), d_base.data_ptr() + r * 256 * 4)
-                e3.record()
-            s.stream.synchronize()
-            evs[r] += [e2, e3]
+        words, ev1 = timed_step(lambda r, s: s.prepare_window(op, ptr, ns, ts))
+        summed(words)
+        bits, ev2 = timed_step(lambda r, s: s.decide_window(*s.home_range(len(ns)), d_res.data_ptr(),
+                                                            d_base.data_ptr() + r * 256 * 4))
+        summed(bits)
+        _, ev3 = timed_step(lambda r, s: s.commit_decided())
         for s in shards:
             s.sync()
         if timed:
-            times.append([(e[0].elapsed_time(e[1]), e[2].elapsed_time(e[3])) for e in evs])
+            times.append([(a[0].elapsed_time(a[1]), b_[0].elapsed_time(b_[1]), c[0].elapsed_time(c[1]))
+                          for a, b_, c in zip(ev1, ev2, ev3)])
         return sum(ns)
 
     nb_acc = (n_acc + BATCH - 1) // BATCH
@@ -104,16 +110,17 @@ def main():
         n = window(Operation.create_transfers, d_x, b0, min(b0 + win, nb), n_x, k >= a.warmup)
         if k >= a.warmup:
             events += n
-    t = np.array(times)  # windows x shards x (prep, commit), ms
+    t = np.array(times)  # windows x shards x (prep, decide, commit), ms
     per_shard = t.sum(axis=2)
     crit = per_shard.max(axis=1).sum() / 1000.0
     out = {
         "shards": G, "window_batches": win, "timed_windows": len(times), "events_timed": events,
         "shard_ms_per_window": {"prep_mean": round(float(t[:, :, 0].mean()), 4),
-                                "commit_mean": round(float(t[:, :, 1].mean()), 4),
+                                "decide_mean": round(float(t[:, :, 1].mean()), 4),
+                                "commit_mean": round(float(t[:, :, 2].mean()), 4),
                                 "max_shard_mean": round(float(per_shard.max(axis=1).mean()), 4)},
         "estimated_rate_excl_collective": round(events / crit, 1),
-        "exchange_bytes_per_window": 16 + 9 * win * BATCH,
+        "exchange_bytes_per_window": 16 + 9 * win * BATCH + 16 + win * BATCH // 8,
         "stats_shard0": shards[0].stats(),
     }
     print(json.dumps(out), flush=True)
