@@ -220,11 +220,12 @@ def cpu_baseline(args, seed):
 def shard_kernel_bytes(kernel, G, prefix):
     """Algorithmic bytes per window event of the sharded scan / apply kernels (csrc/shard.h)."""
     if kernel == "prep":
-        # k_sh_scan_ct: ids + amount 64, facts 9, scratch 13; the rest of the record (64) for events
-        # with an owned role (1 - (1 - 1/G)^3 of them); owned probes: 2 account-table entries 2 x 32,
-        # key-map claim 16 (fresh monotonic ids skip the transfer-id probe)
+        # k_sh_owned_ct, per window event: the events with an owned role (1 - (1 - 1/G)^3 of them)
+        # are read whole (128) with their list entry (4 read + 4 written) and facts (9) and slots
+        # (8); owned probes: 2 account-table entries 2 x 32, key-map claim 16 (fresh monotonic ids
+        # skip the transfer-id probe)
         p_own = 1.0 - (1.0 - 1.0 / G) ** 3
-        return 64 + 9 + 13 + 64 * p_own + (2 * 32 + 16) / G
+        return p_own * (128 + 8 + 9 + 8) + (2 * 32 + 16) / G
     # k_sh_apply: roles byte + commit bit; owned: per balance side amount 16 + slot 4 + balance
     # read+write 64, record read + append 2 x 128, id-table entry 32 unless the window extends the
     # sorted prefix
@@ -351,7 +352,7 @@ def run_sharded(args, torch, dist, world, rank, device):
             prefix = st["sorted_transfers"] == st["transfers"]
             bytes_launch = int(shard_kernel_bytes(dom, G, prefix) * ev_per_launch)
             achieved = bytes_launch / (us * 1e-6) / 1e9
-            kname = {"prep": "k_sh_scan_ct", "final": "k_sh_apply<true>"}[dom]
+            kname = {"prep": "k_sh_owned_ct", "final": "k_sh_apply<true>"}[dom]
             tr = pmc_traffic("cfg5", kname, ev_per_launch) if G == 1 else None
             roof = {"bound": "hbm", "kernel": kname, "events_per_launch": int(ev_per_launch),
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
