@@ -89,15 +89,30 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
   if (!cpw_active(g)) return;
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j == 0) g->cpw_done = 1;
-  if (j >= g->cc_count) return;
-  const uint32_t start = s.cc_list[j];
-  const uint32_t key = s.rkey[start];
-  uint32_t len = 1;
-  while (start + len < w.E && s.rkey[start + len] == key) len++;
-  // statistics (tbg_debug_counters): [5] longest component, [6] components, [7] W events walked
-  atomicMax((unsigned long long*)&g->dbg[5], (unsigned long long)len);
-  atomicAdd((unsigned long long*)&g->dbg[6], 1ull);
-  atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)len);
+  const bool on = j < g->cc_count;
+  uint32_t start = 0, len = 0;
+  if (on) {
+    start = s.cc_list[j];
+    const uint32_t key = s.rkey[start];
+    len = 1;
+    while (start + len < w.E && s.rkey[start + len] == key) len++;
+  }
+  // statistics (tbg_debug_counters): [5] longest component, [6] components, [7] W events walked;
+  // one lane per wave adds (same-address atomics from every component serialize at the memory side)
+  uint32_t mx = len, sum = len;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t y = __shfl_xor(mx, o, 64);
+    mx = y > mx ? y : mx;
+    sum += __shfl_xor(sum, o, 64);
+  }
+  const uint32_t n_on = (uint32_t)__popcll(__ballot(on));
+  if ((threadIdx.x & 63) == 0 && n_on) {
+    atomicMax((unsigned long long*)&g->dbg[5], (unsigned long long)mx);
+    atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)n_on);
+    atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)sum);
+  }
+  if (!on) return;
   Walker wk;
   wk.d = d;
   wk.s = s;

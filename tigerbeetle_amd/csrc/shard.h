@@ -275,8 +275,12 @@ __global__ void __launch_bounds__(SEG) k_sh_roles(Dev d, Scratch s, const uint8_
   }
 }
 
-// Owned work of segment blockIdx.x: validation, the owned probes / claim / exists, the owner facts.
-// Rewrites each entry's roles to the validated ones (0 unless the event reaches the account checks).
+// Owned work of segment blockIdx.x: the owner facts. The id owner reads the event whole, validates
+// it and, if it reaches the account checks, claims the id and compares it with a stored transfer.
+// The account owners need no validation: they read the account ids and the amount only (facts of an
+// event its home rejects statically are never read, and the commit bit gates every effect); every
+// amount they see counts toward the overflow bound, valid or not. Rewrites each entry's roles to the
+// ones that carry effects.
 __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
                                                      uint32_t epoch, XchView xch) {
   __shared__ u128 red[SEG / 64];
@@ -290,35 +294,14 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
   if (threadIdx.x < n) {
     const uint32_t x = s.wlist[k];
     const uint32_t i = ol_event(x), cand = ol_roles(x);
-    tb_transfer_t t = ev[i];
-    uint32_t cls = 0, roles = 0, drl = 0, crl = 0, zw = 0;
-    bool reach, unsup;
-    (void)sh_static_ct(t, w, win_batch(w, i), i, &cls, &reach, &unsup);
-    if (reach) {
-      roles = cand;
-      if (cand & (ROLE_DR | ROLE_CR)) amount_upper = U(t.amount);
-      // up to three independent probes, one per owned side
-      if (cand & ROLE_DR) {
-        AccEntry e;
-        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, t.debit_account_id, &e);
-        s.dr_slot[i] = slot;
-        if (slot != NONE32) {
-          drl = e.ledger;
-          if (e.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) zw |= SH_DR_LIMIT;
-        }
-        xch.drl[i] = drl;
-      }
-      if (cand & ROLE_CR) {
-        AccEntry e;
-        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, t.credit_account_id, &e);
-        s.cr_slot[i] = slot;
-        if (slot != NONE32) {
-          crl = e.ledger;
-          if (e.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) zw |= SH_CR_LIMIT;
-        }
-        xch.crl[i] = crl;
-      }
-      if (cand & ROLE_ID) {
+    uint32_t roles = 0, zw = 0;
+    if (cand & ROLE_ID) {
+      tb_transfer_t t = ev[i];
+      uint32_t cls = 0;
+      bool reach, unsup;
+      (void)sh_static_ct(t, w, win_batch(w, i), i, &cls, &reach, &unsup);
+      if (reach) {
+        roles |= ROLE_ID;
         atomicAdd(&aux, 1u << SHX_OWN_SHIFT);
         bool dup;
         (void)sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
@@ -330,8 +313,38 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
         }
         zw |= 1 + (xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]));
       }
-      xch.zw[i] = (uint8_t)zw;
     }
+    if (cand & (ROLE_DR | ROLE_CR)) {
+      const uint4* q = reinterpret_cast<const uint4*>(ev + i);
+      const uint4 q1 = q[1], q2 = q[2], q3 = q[3];
+      amount_upper = U(rw_u128(q3));
+      // up to two independent probes, one per owned side
+      if (cand & ROLE_DR) {
+        roles |= ROLE_DR;
+        AccEntry e;
+        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, rw_u128(q1), &e);
+        s.dr_slot[i] = slot;
+        uint32_t drl = 0;
+        if (slot != NONE32) {
+          drl = e.ledger;
+          if (e.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) zw |= SH_DR_LIMIT;
+        }
+        xch.drl[i] = drl;
+      }
+      if (cand & ROLE_CR) {
+        roles |= ROLE_CR;
+        AccEntry e;
+        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, rw_u128(q2), &e);
+        s.cr_slot[i] = slot;
+        uint32_t crl = 0;
+        if (slot != NONE32) {
+          crl = e.ledger;
+          if (e.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) zw |= SH_CR_LIMIT;
+        }
+        xch.crl[i] = crl;
+      }
+    }
+    if (zw) xch.zw[i] = (uint8_t)zw;
     s.wlist[k] = i | (roles << 24);
   }
   if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&aux, (uint32_t)SHX_HUGE);
@@ -580,13 +593,13 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
       if (drs != NONE32 && !sh_guard(g, drs < d.acc_max, 3, drs)) drs = NONE32;
       if (crs != NONE32 && !sh_guard(g, crs < d.acc_max, 4, crs)) crs = NONE32;
       if (ins && !sh_guard(g, xbase + rins < d.x_max, 5, xbase + rins)) ins = false;
-      tb_transfer_t t2 = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
-      const u128 a = U(t2.amount);
+      const u128 a = U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].amount);
       Add128 a_dr, a_cr;
       if (drs != NONE32) a_dr.issue(&d.acc[drs].debits_posted, a, small);
       if (crs != NONE32) a_cr.issue(&d.acc[crs].credits_posted, a, small);
       if (ins) {
         const uint64_t slot = xbase + rins;
+        tb_transfer_t t2 = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
         t2.timestamp = win_ts(w, win_batch(w, i), i);
         d.xr[slot] = t2;
         if (!prefix_win) x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
