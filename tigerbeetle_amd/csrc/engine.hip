@@ -358,11 +358,13 @@ __global__ void __launch_bounds__(256) k_ca_prep(Dev d, Scratch s, const tb_acco
 // ------------------------------------------------------------------------------------------------
 // U: the event's outcome depends on order or state.
 template <bool XFER>
-__device__ inline bool is_u(const Scratch& s, uint32_t j, uint32_t cls, uint32_t epoch, bool ovf_mode) {
+__device__ inline bool is_u(const Scratch& s, uint32_t j, uint32_t cls, uint32_t epoch, bool ovf_mode,
+                            bool claim_free) {
   if (!(cls & C_REACH)) return false;
-  const uint32_t e = s.id_ent[j];
-  if (!XFER) return bmap_idc(s.bmap, e, epoch) > 1;  // duplicate account id in the window
+  if (!XFER) return bmap_idc(s.bmap, s.id_ent[j], epoch) > 1;  // duplicate account id in the window
   if (ovf_mode || (cls & (C_READS_DR | C_READS_CR))) return true;
+  if (claim_free) return false;  // no id repeats and no post/void in the window (k_prep_reduce)
+  const uint32_t e = s.id_ent[j];
   // duplicate transfer id, or a post/void in the window targets this id
   if (bmap_idc(s.bmap, e, epoch) > 1 || bmap_pidc(s.bmap, e, epoch) > 0) return true;
   if (cls & C_POSTVOID) {
@@ -375,12 +377,13 @@ __device__ inline bool is_u(const Scratch& s, uint32_t j, uint32_t cls, uint32_t
 
 // W: runs on the walker (U, or touches an account some U event reads).
 template <bool XFER>
-__device__ inline bool is_w(const Dev& d, const Scratch& s, uint32_t j, uint32_t* cls, uint32_t epoch, bool ovf_mode) {
-  if (is_u<XFER>(s, j, *cls, epoch, ovf_mode)) {
+__device__ inline bool is_w(const Dev& d, const Scratch& s, uint32_t j, uint32_t* cls, uint32_t epoch, bool ovf_mode,
+                            bool claim_free, bool any_hot) {
+  if (is_u<XFER>(s, j, *cls, epoch, ovf_mode, claim_free)) {
     *cls |= C_U;
     return true;
   }
-  if (!XFER || !(*cls & C_REACH)) return false;
+  if (!XFER || !(*cls & C_REACH) || !any_hot) return false;
   const uint32_t dr = s.dr_slot[j], cr = s.cr_slot[j];
   return (dr != NONE32 && d.hot[dr] == epoch) || (cr != NONE32 && d.hot[cr] == epoch);
 }
@@ -395,7 +398,7 @@ __device__ inline bool res_bad(const Scratch& s, uint32_t j, uint32_t cls, uint3
 
 template <bool XFER>
 __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinDesc& w, uint32_t i, uint32_t epoch,
-                                      bool ovf_mode) {
+                                      bool ovf_mode, bool claim_free, bool any_hot) {
   const uint32_t b = s.batch[i];
   const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
   uint32_t cls = s.cls[i];
@@ -403,7 +406,7 @@ __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinD
   if (i != first && (s.cls[i - 1] & C_LINKED)) return false;  // chain member: its head decides
   if (!linked) {
     // singleton (:1255-1259, :1289-1290)
-    if (is_w<XFER>(d, s, i, &cls, epoch, ovf_mode)) {
+    if (is_w<XFER>(d, s, i, &cls, epoch, ovf_mode, claim_free, any_hot)) {
       s.cls[i] = cls | C_W;
       return res_bad(s, i, cls, epoch);
     }
@@ -417,7 +420,7 @@ __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinD
   uint32_t f = NONE32;
   for (uint32_t j = i;; j++) {
     uint32_t cj = s.cls[j];
-    if (is_w<XFER>(d, s, j, &cj, epoch, ovf_mode)) any_w = true;
+    if (is_w<XFER>(d, s, j, &cj, epoch, ovf_mode, claim_free, any_hot)) any_w = true;
     const bool lj = cj & C_LINKED;
     const uint32_t code = (lj && j == last) ? (uint32_t)TB_CT_LINKED_EVENT_CHAIN_OPEN : s.code[j];
     if (code != TB_CT_OK && f == NONE32) f = j;
@@ -447,7 +450,11 @@ __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, u
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool ovf_mode = XFER && window_ovf_mode(d.g);
   bool bad = false;
-  if (i < w.E) bad = classify_event<XFER>(d, s, w, i, epoch, ovf_mode);
+  // transfer windows: claim-free (k_prep_reduce) skips the key-map reads, no hot account skips the
+  // hot-mark reads
+  const bool claim_free = XFER && (d.g->win_flags & 1u) != 0;
+  const bool any_hot = !XFER || d.g->hot_count != 0;
+  if (i < w.E) bad = classify_event<XFER>(d, s, w, i, epoch, ovf_mode, claim_free, any_hot);
   if (XFER && i == 0) {
     // the resolver's 128-bit signed arithmetic needs every balance sum below 2^126
     const u128 sum = d.g->ovf_bound + d.g->batch_amount_sum;
