@@ -121,5 +121,6 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
   wk.w = &w;
   wk.epoch = epoch;
   wk.atomic_bal = true;
+  wk.small_bal = g->small_win != 0;  // k_prep_reduce
   wk.template run<XFER>(s.rval + start, len);
 }

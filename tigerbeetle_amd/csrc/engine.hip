@@ -284,6 +284,10 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
     const bool claim_free = !(aux & 2u);
     const bool prefix = claim_free && (aux & 4u) && g->x_sorted == g->x_count;
     g->win_flags = (claim_free ? 1u : 0u) | (prefix ? 2u : 0u);
+    // every balance field stays below 2^64 this window (k_walk computes the same for k_final; the
+    // component walkers, which run before k_walk, read it from here)
+    const u128 sum = g->ovf_bound + g->batch_amount_sum;
+    g->small_win = !g->batch_huge && sum >= g->ovf_bound && (uint64_t)(sum >> 64) == 0;
   }
 }
 

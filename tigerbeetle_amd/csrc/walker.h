@@ -75,6 +75,10 @@ struct Walker {
   // used in windows where no decision reads a balance (no hot account, no overflow risk), so the
   // racy balance values read below never change an outcome.
   bool atomic_bal;
+  // With atomic_bal: the window keeps every balance field below 2^64 (Globals::small_win), so a
+  // balance delta is a no-return 64-bit add on the low word (mod 2^64; the true value never leaves
+  // the low word) and no walker waits for an atomic's result.
+  bool small_bal = false;
 
   __device__ void log_bal(uint32_t slot) {
     if (!scope) return;
@@ -98,7 +102,10 @@ struct Walker {
     return f == 0 ? &a->debits_pending : f == 1 ? &a->debits_posted : f == 2 ? &a->credits_pending : &a->credits_posted;
   }
   __device__ void add_bal(uint32_t slot, uint32_t f, u128 v) {
-    atomic_add_u128(bal_field(&d.acc[slot], f), v);
+    if (small_bal)
+      (void)atomicAdd(reinterpret_cast<unsigned long long*>(bal_field(&d.acc[slot], f)), (unsigned long long)v);
+    else
+      atomic_add_u128(bal_field(&d.acc[slot], f), v);
     if (!scope) return;
     UndoRec& r = s.undo[undo_n++];
     r.kind = UNDO_ADD;
@@ -110,7 +117,13 @@ struct Walker {
     while (undo_n) {
       const UndoRec& r = s.undo[--undo_n];
       switch (r.kind) {
-        case UNDO_ADD: atomic_add_u128(bal_field(&d.acc[r.a], r.pad0), (u128)0 - r.old[0]); break;
+        case UNDO_ADD:
+          if (small_bal)
+            (void)atomicAdd(reinterpret_cast<unsigned long long*>(bal_field(&d.acc[r.a], r.pad0)),
+                            (unsigned long long)((u128)0 - r.old[0]));
+          else
+            atomic_add_u128(bal_field(&d.acc[r.a], r.pad0), (u128)0 - r.old[0]);
+          break;
         case UNDO_BAL: {
           Bal b;
           b.dp = r.old[0];
