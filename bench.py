@@ -122,6 +122,8 @@ def parse():
     p.add_argument("--resolver", default="relax", choices=["relax", "wait", "off"],
                    help="balance-limit windows: windowed relaxation (default), wait-based walkers, walker only")
     p.add_argument("--verify", action="store_true", help="setup all ok; cfg1/cfg2: every transfer ok")
+    p.add_argument("--change-log", action="store_true",
+                   help="engine keeps the write-back change log (TBG_FLAG_CHANGE_LOG): its device cost")
     a = p.parse_args()
     if a.config is None:
         a.config = "cfg5" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "cfg2"
@@ -441,7 +443,8 @@ def main():
 
     sm = StateMachine(device=device, batch_max=BATCH, accounts_max=n_acc_total, transfers_max=n_xfer + n_setup,
                       window_events_max=win * BATCH,
-                      resolver={"relax": True, "wait": "wait", "off": False}[args.resolver])
+                      resolver={"relax": True, "wait": "wait", "off": False}[args.resolver],
+                      change_log=args.change_log)
     stream = sm.stream
     ext = torch.cuda.ExternalStream(stream)
 
@@ -603,7 +606,7 @@ def main():
             "dtype": "u128",
             "data": "synthetic (device-generated, seed %d)" % args.seed,
             "config": {"workload": desc, "batch": BATCH, "window_batches": win, "accounts_per_gpu": n_acc,
-                       "transfers_per_gpu": n_xfer, "resolver": args.resolver,
+                       "transfers_per_gpu": n_xfer, "resolver": args.resolver, "change_log": bool(args.change_log),
                        "parallelism": "independent account shards" if world > 1 else "single GPU"},
             "results": {"failed_events_timed": int(all_fails),
                         "ok_events_per_s": round((all_events - all_fails) / elapsed, 1),

@@ -95,6 +95,14 @@ enum {
     TB_PENDING_EXPIRED = 4
 };
 
+/* TransferPending groove object (state_machine.zig:259-269): keyed by the pending transfer's
+ * timestamp. 16 B. */
+typedef struct tb_transfer_pending_t {
+    uint64_t timestamp;
+    uint8_t status;  /* TB_PENDING_* */
+    uint8_t padding[7];
+} tb_transfer_pending_t;
+
 /* Operation (state_machine.zig:341-350). */
 enum {
     TB_OP_PULSE = 128,

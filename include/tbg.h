@@ -36,6 +36,9 @@ typedef struct tbg_config {
     uint32_t shard_index;    /* this engine's shard, < shard_count */
 } tbg_config;
 
+/* Keep a change log of each committed create_* window (tbg_window_changes): the write-back stream
+   to the LSM forest. Costs three small kernels per window; off by default. */
+#define TBG_FLAG_CHANGE_LOG 8u
 /* Decide balance-limit windows on the sequential walker only (no account-parallel resolver). */
 #define TBG_FLAG_NO_RESOLVER 1u
 /* Walk W events on the single sequential walker only (no component-parallel walkers). */
@@ -149,6 +152,17 @@ int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
 
 /* Debug: cumulative resolver counters (see host.inc); up to 8 values. */
 int tbg_debug_counters(tbg_engine *engine, uint64_t *out, uint32_t n);
+
+/* Write-back stream of the last committed create_* window (TBG_FLAG_CHANGE_LOG; state_machine.zig
+ * groove side effects: groove.insert/update, lsm/groove.zig:905-1000): every account record the
+ * window created or whose balances it changed (current values, ascending creation order), every
+ * transfer record it inserted (commit order), and the TransferPending rows it inserted or updated
+ * (new pending transfers, and earlier ones it posted or voided; ascending timestamp). Synchronous.
+ * TBG_E_CAPACITY if a buffer is too small (the counts are still written); TBG_E_STATE without the
+ * flag. */
+int tbg_window_changes(tbg_engine *engine, tb_account_t *accounts, uint64_t accounts_cap, uint64_t *accounts_count,
+                       tb_transfer_t *transfers, uint64_t transfers_cap, uint64_t *transfers_count,
+                       tb_transfer_pending_t *pending, uint64_t pending_cap, uint64_t *pending_count);
 
 /* Whole-state dumps in creation (= timestamp) order, for parity checks. */
 int tbg_dump_accounts(tbg_engine *engine, tb_account_t *out, uint64_t cap, uint64_t *count);

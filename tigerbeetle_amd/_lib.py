@@ -17,7 +17,7 @@ EXPORTS = [
     "tbg_timing_enable", "tbg_timing_collect", "tbg_gen_accounts_cfg3", "tbg_gen_funding_cfg3",
     "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4", "tbg_debug_counters", "tbg_shard_of",
     "tbg_shard_prepare_window", "tbg_shard_decide_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
-    "tbg_shard_commit_bits_bytes",
+    "tbg_shard_commit_bits_bytes", "tbg_window_changes",
 ]
 
 
@@ -39,6 +39,7 @@ class Config(ctypes.Structure):
 FLAG_NO_RESOLVER = 1
 FLAG_NO_COMPONENTS = 2
 FLAG_RES_WAIT = 4
+FLAG_CHANGE_LOG = 8
 
 
 class Stats(ctypes.Structure):
@@ -101,6 +102,7 @@ def lib():
         "tbg_shard_decide_window": ([vp, vp, u32, u32, vp, vp, vp], i32),
         "tbg_shard_commit_window": ([vp, vp, vp], i32),
         "tbg_shard_commit_bits_bytes": ([u32], u64),
+        "tbg_window_changes": ([vp, vp, u64, P(u64), vp, u64, P(u64), vp, u64, P(u64)], i32),
         "tbg_shard_exchange_bytes": ([u32, u32], u64),
     }
     for name, (args, res) in sig.items():

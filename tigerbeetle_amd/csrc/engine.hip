@@ -41,6 +41,7 @@
 #include "resolver.h"
 #include "relax.h"
 #include "window.h"
+#include "changes.h"
 
 // Probe continuation after a first entry was already loaded (lets the first probes of several
 // independent lookups be in flight together).

@@ -12,6 +12,8 @@ import numpy as np
 from . import _lib
 from .types import ACCOUNT_DTYPE, BATCH_MAX, TRANSFER_DTYPE, Operation
 
+PENDING_ROW_DTYPE = np.dtype([("timestamp", "<u8"), ("status", "u1"), ("padding", "u1", (7,))])  # 16 B
+
 MESSAGE_BODY_SIZE_MAX = 1048576 - 256
 
 
@@ -27,12 +29,13 @@ def to_host(t):
 
 class StateMachine:
     def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20,
-                 window_events_max=0, resolver=True, components=True, shard_count=0, shard_index=0):
+                 window_events_max=0, resolver=True, components=True, shard_count=0, shard_index=0,
+                 change_log=False):
         L = _lib.lib()
         # resolver: True/"relax" = windowed relaxation (relax.h), "wait" = wait-based walkers
         # (resolver.h), False = sequential walker only
         flags = ((0 if resolver else _lib.FLAG_NO_RESOLVER) | (0 if components else _lib.FLAG_NO_COMPONENTS) |
-                 (_lib.FLAG_RES_WAIT if resolver == "wait" else 0))
+                 (_lib.FLAG_RES_WAIT if resolver == "wait" else 0) | (_lib.FLAG_CHANGE_LOG if change_log else 0))
         cfg = _lib.Config(device, batch_max, accounts_max, transfers_max, window_events_max, flags, shard_count,
                           shard_index)
         h = ctypes.c_void_p()
@@ -96,6 +99,24 @@ class StateMachine:
         s = _lib.Stats()
         _lib.check(_lib.lib().tbg_get_stats(self.h, ctypes.byref(s)), "stats")
         return {f: getattr(s, f) for f, _ in _lib.Stats._fields_}
+
+    def window_changes(self):
+        """Write-back stream of the last committed create_* window (include/tbg.h tbg_window_changes):
+        (changed/new account records, inserted transfer records, TransferPending rows as a structured
+        array of (timestamp, status))."""
+        L = _lib.lib()
+        na, nt, npd = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        rc = L.tbg_window_changes(self.h, None, 0, ctypes.byref(na), None, 0, ctypes.byref(nt), None, 0,
+                                  ctypes.byref(npd))
+        if rc not in (0, -2):
+            _lib.check(rc, "window_changes")
+        acc = np.zeros(na.value, ACCOUNT_DTYPE)
+        xfer = np.zeros(nt.value, TRANSFER_DTYPE)
+        rows = np.zeros(npd.value, PENDING_ROW_DTYPE)
+        _lib.check(L.tbg_window_changes(self.h, acc.ctypes.data, len(acc), ctypes.byref(na), xfer.ctypes.data,
+                                        len(xfer), ctypes.byref(nt), rows.ctypes.data, len(rows),
+                                        ctypes.byref(npd)), "window_changes")
+        return acc, xfer, rows
 
     def pulse_next_timestamp(self):
         return self.stats()["pulse_next_timestamp"]
