@@ -153,11 +153,12 @@ int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
 /* Debug: cumulative resolver counters (see host.inc); up to 8 values. */
 int tbg_debug_counters(tbg_engine *engine, uint64_t *out, uint32_t n);
 
-/* Write-back stream of the last committed create_* window (TBG_FLAG_CHANGE_LOG; state_machine.zig
- * groove side effects: groove.insert/update, lsm/groove.zig:905-1000): every account record the
- * window created or whose balances it changed (current values, ascending creation order), every
- * transfer record it inserted (commit order), and the TransferPending rows it inserted or updated
- * (new pending transfers, and earlier ones it posted or voided; ascending timestamp). Synchronous.
+/* Write-back stream of the last commit call (TBG_FLAG_CHANGE_LOG; state_machine.zig groove side
+ * effects: groove.insert/update, lsm/groove.zig:905-1000), covering its pulse and its create_*
+ * window: every account record whose balances they changed (current values, ascending creation
+ * order) followed by the accounts the window created, every transfer record it inserted (commit
+ * order), and the TransferPending rows inserted or updated (new pending transfers, earlier ones
+ * posted, voided or expired; ascending timestamp). Unsharded engines. Synchronous.
  * TBG_E_CAPACITY if a buffer is too small (the counts are still written); TBG_E_STATE without the
  * flag. */
 int tbg_window_changes(tbg_engine *engine, tb_account_t *accounts, uint64_t accounts_cap, uint64_t *accounts_count,

@@ -9,7 +9,8 @@
 //     (k_chg_mark; plain stores, every writer stores the same value), then listed in slot order
 //     (k_chg_count, k_chg_scan, k_chg_list);
 //   - earlier pending transfers that a committed post/void resolved are listed by k_chg_mark.
-// tbg_window_changes gathers and copies them. Pulse (expiry) changes are not logged.
+// k_pulse_apply marks the accounts and lists the transfers of every expiry the same way. A commit
+// call's log covers its pulse (if any) and its window. tbg_window_changes gathers and copies them.
 #pragma once
 #include "window.h"
 

@@ -962,7 +962,8 @@ __global__ void __launch_bounds__(1024) k_pulse_select(Dev d, Scratch s, PulseCt
   }
 }
 
-__global__ void __launch_bounds__(256) k_pulse_apply(Dev d, Scratch s, const PulseCtl* ctl) {
+__global__ void __launch_bounds__(256) k_pulse_apply(Dev d, Scratch s, const PulseCtl* ctl, ChgLog chg,
+                                                     uint32_t chg_epoch) {
   if (!ctl->active) return;
   const uint32_t m = d.g->cand_count;
   const uint32_t cur = *d.exp_cur;
@@ -984,6 +985,11 @@ __global__ void __launch_bounds__(256) k_pulse_apply(Dev d, Scratch s, const Pul
     atomic_sub_u128(&d.acc[drs].debits_pending, amt);
     atomic_sub_u128(&d.acc[crs].credits_pending, amt);
     d.xstatus[e.slot] = TB_PENDING_EXPIRED;
+    if (chg.mark) {  // change log (changes.h): both accounts and the expired TransferPending row
+      chg.mark[drs] = chg_epoch;
+      chg.mark[crs] = chg_epoch;
+      chg.pend[atomicAdd(&chg.cnt[1], 1u)] = e.slot;
+    }
   }
 }
 
