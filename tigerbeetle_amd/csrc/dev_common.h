@@ -117,10 +117,6 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t mono_prev;   // the previous transfer window was claim-free (k_ct_prep's speculation)
   uint64_t x_id_max;    // >= every stored transfer id (u64 max once any id needs > 64 bits): an id
                         // above it cannot exist, so its table probe is skipped (monotonic ids)
-  // sharded engines (shard.h), per window
-  uint32_t sh_blocks;   // prep blocks finished (the last one closes the trailer word)
-  uint32_t sh_unsup;    // the window is outside the sharded class: nothing is applied
-  uint64_t sh_own;      // events this shard owns the id of (capacity check)
 };
 
 // Per-event class bits (scratch `cls`).

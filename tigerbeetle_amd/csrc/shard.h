@@ -9,11 +9,12 @@
 //   k_sh_roles    whole window: the ids of each event (64 B); events with a role this shard owns
 //                 (debit account, credit account, transfer id) are compacted, in event order, into
 //                 per-segment lists, so the owned work below runs on dense waves.
-//   k_sh_owned_*  owned events only: read whole and validated (state_machine.zig:1424-1439,
-//                 1465-1489); for those that reach the account checks the owner resolves its side:
-//                 the debit / credit account (ledger, limit flag), or the transfer id (pre-window
-//                 `exists` comparison :1506-1507, in-window duplicates through the window key map).
-//                 Each owner writes its part of the event's 9 B of facts (exchange 1).
+//   k_sh_owned_*  owned events only: the id owner reads the event whole and validates it
+//                 (state_machine.zig:1424-1439, 1465-1489); if it reaches the account checks, it
+//                 claims the id (in-window duplicates through the window key map) and compares it
+//                 with a stored transfer (`exists`, :1506-1507). The debit / credit owners read the
+//                 account ids and the amount and resolve their account (ledger, limit flag). Each
+//                 owner writes its part of the event's 9 B of facts (exchange 1).
 //   k_sh_close    one block: folds the scan blocks' partials (capacity, overflow bound, prefix flag).
 //   (caller)      exchange 1: byte-wise sum all-reduce of the facts (RCCL over xGMI). Every bit has
 //                 exactly one writer, so the sum is the union.
@@ -115,9 +116,9 @@ __device__ inline uint32_t sh_claim(Globals* g, BEntry* bm, uint32_t mask, const
   }
 }
 
-// End-of-window device state (the last event's thread of k_sh_final). Nothing written here is read
-// by k_sh_final's other blocks, which may still be running: their store base is Globals::base
-// (captured by k_sh_count) and sh_unsup is cleared by the next window's k_sh_close.
+// End-of-window device state (thread 0 of k_sh_apply's last block). Nothing written here is read
+// by k_sh_apply's other blocks, which may still be running: their store base is Globals::base
+// (captured by k_sh_icount).
 __device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bool apply) {
   if (apply) {
     if (xfer) {
