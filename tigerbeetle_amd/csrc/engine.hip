@@ -43,6 +43,34 @@
 #include "window.h"
 #include "changes.h"
 
+// k_final's streams, nontemporal: the window's event records (read for the last time) and the
+// inserted transfer records pass by, while the account table and records stay cached across windows
+// (A/B on one box, cfg2: +1.5-2 % transfers/s, prep 155 -> 148 us per 1M events; k_ct_prep's own
+// event loads are 8 strided 16 B loads per lane and get slower nontemporal, 155 -> 189 us).
+#ifndef TBG_NT_LOAD
+#define TBG_NT_LOAD 1
+#endif
+#ifndef TBG_NT_STORE
+#define TBG_NT_STORE 1
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
+#if TBG_NT_LOAD
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void st_stream(uint4* p, uint4 v) {
+#if TBG_NT_STORE
+  const u32x4_t x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4_t*>(p));
+#else
+  *p = v;
+#endif
+}
+
 // Probe continuation after a first entry was already loaded (lets the first probes of several
 // independent lookups be in flight together).
 __device__ inline uint32_t acc_probe_from(const AccEntry* __restrict__ tab, uint64_t mask, uint64_t h, AccEntry e,
@@ -687,7 +715,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
 #pragma unroll
     for (uint32_t q = 0; q < 8; q++) {
       const uint32_t k = q * 64 + lane;
-      if ((k >> 3) < nrec) ws[k] = src[k];
+      if ((k >> 3) < nrec) ws[k] = ld_stream(src + k);
     }
   }
   uint32_t cls = 0, code = TB_CT_OK;
@@ -822,7 +850,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   wave_sync();
   if (!(o.xskip & 4)) {
     uint4* dst = reinterpret_cast<uint4*>(XFER ? (void*)d.xr : (void*)d.acc) + (size_t)(xbase + r0) * 8;
-    for (uint32_t k = lane; k < nins * 8; k += 64) dst[k] = ws[k];
+    for (uint32_t k = lane; k < nins * 8; k += 64) st_stream(dst + k, ws[k]);
   }
   if (i == E - 1) {
     // the window's last event: totals and window-level state
