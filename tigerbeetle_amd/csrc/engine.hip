@@ -325,13 +325,15 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
 __global__ void __launch_bounds__(256) k_claim_fix(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, uint32_t E,
                                                    uint32_t epoch) {
   if (!d.g->mono_prev || (d.g->win_flags & 1u)) return;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E) return;
-  const uint32_t cls = s.cls[i];
-  if (!(cls & C_REACH)) return;
+  // grid-stride over a capped grid: the common case (speculation right) is a launch whose blocks
+  // exit at once, so it pays for few blocks
   const uint8_t* evb = reinterpret_cast<const uint8_t*>(ev);
-  s.id_ent[i] = bmap_claim(s.bmap, s.bmask, evb, ev[i].id, i, 0, epoch);
-  if (cls & C_POSTVOID) s.pid_ent[i] = bmap_claim(s.bmap, s.bmask, evb, ev[i].pending_id, i, 1, epoch);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x) {
+    const uint32_t cls = s.cls[i];
+    if (!(cls & C_REACH)) continue;
+    s.id_ent[i] = bmap_claim(s.bmap, s.bmask, evb, ev[i].id, i, 0, epoch);
+    if (cls & C_POSTVOID) s.pid_ent[i] = bmap_claim(s.bmap, s.bmask, evb, ev[i].pending_id, i, 1, epoch);
+  }
 }
 
 
