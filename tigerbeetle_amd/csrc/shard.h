@@ -560,6 +560,8 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
                                                   const unsigned long long* bits) {
   __shared__ uint32_t lds[SEG / 64];
   __shared__ unsigned long long ldsm[SEG / 64];
+  // inserted transfer records, compacted per wave and stored as one contiguous run (as in k_final)
+  __shared__ uint4 stage[XFER ? SEG * 8 : 1];
   Globals* g = d.g;
   const bool last_block = blockIdx.x == gridDim.x - 1;
   if (sh_abort(trailer1, trailer2)) {
@@ -588,6 +590,7 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
     const unsigned long long m = block_max_u64<SEG / 64>(key, ldsm);
     if (threadIdx.x == 0 && m > g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&g->x_id_max), m);
   }
+  const uint32_t r0 = __shfl(rins, 0);  // the wave's first insert rank (all lanes active here)
   if (commit) {
     if (XFER) {
       uint32_t drs = (roles & ROLE_DR) ? s.dr_slot[i] : NONE32, crs = (roles & ROLE_CR) ? s.cr_slot[i] : NONE32;
@@ -602,7 +605,12 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
         const uint64_t slot = xbase + rins;
         tb_transfer_t t2 = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
         t2.timestamp = win_ts(w, win_batch(w, i), i);
-        d.xr[slot] = t2;
+        // ranks of a wave's inserts are consecutive (block_excl); a failed slot guard can only drop
+        // a suffix of them, so the staged run below stays gap-free
+        const uint4* tw = reinterpret_cast<const uint4*>(&t2);
+        uint4* ws = stage + (threadIdx.x >> 6) * 512;
+#pragma unroll
+        for (int q = 0; q < 8; q++) ws[(rins - r0) * 8 + q] = tw[q];
         if (!prefix_win) x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
         d.xstatus[slot] = 0;
       }
@@ -615,6 +623,15 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
       d.acc[slot] = a;
       d.hot[slot] = 0;
       acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
+    }
+  }
+  if (XFER) {
+    const uint32_t nins = (uint32_t)__popcll(__ballot(ins));
+    wave_sync();
+    if (nins) {
+      const uint4* ws = stage + (threadIdx.x >> 6) * 512;
+      uint4* dst = reinterpret_cast<uint4*>(d.xr) + (size_t)(xbase + r0) * 8;
+      for (uint32_t k = threadIdx.x & 63; k < nins * 8; k += 64) st_stream(dst + k, ws[k]);
     }
   }
   if (last_block && threadIdx.x == 0) {
