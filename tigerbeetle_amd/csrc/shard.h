@@ -289,9 +289,17 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
   const uint32_t k = blockIdx.x * SEG + threadIdx.x;
   if (threadIdx.x == 0) aux = 0;
   if (k == 0) check_window(w, d.g);
-  __syncthreads();
+  // Window ids strictly increasing (k_sh_roles' per-segment bits, one launch per segment here too):
+  // no in-window duplicate id can exist, so the id owner skips the key-map claim, a returning CAS per
+  // owned id (the sharded path reads the key map for nothing else). Other blocks may be OR-ing
+  // their own bits into these words meanwhile; bit SHX_NONMONO is never among them.
+  uint32_t nm = 0;
+  for (uint32_t j = threadIdx.x; j < gridDim.x; j += SEG)
+    nm |= __hip_atomic_load(&s.blk_aux[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & (uint32_t)SHX_NONMONO;
+  const bool mono = !__syncthreads_or((int)nm);
   u128 amount_upper = 0;
   const uint32_t n = s.cnt_w[blockIdx.x];
+  bool owned_id = false;
   if (threadIdx.x < n) {
     const uint32_t x = s.wlist[k];
     const uint32_t i = ol_event(x), cand = ol_roles(x);
@@ -303,9 +311,9 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
       (void)sh_static_ct(t, w, win_batch(w, i), i, &cls, &reach, &unsup);
       if (reach) {
         roles |= ROLE_ID;
-        atomicAdd(&aux, 1u << SHX_OWN_SHIFT);
-        bool dup;
-        (void)sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
+        owned_id = true;
+        bool dup = false;
+        if (!mono) (void)sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
         if (dup) atomicOr(&aux, (uint32_t)SHX_DUP);
         uint32_t xs = NONE32;
         if (x_may_exist(t.id, d.g->x_id_max)) {
@@ -349,6 +357,10 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
     s.wlist[k] = i | (roles << 24);
   }
   if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&aux, (uint32_t)SHX_HUGE);
+  {  // owned ids reaching the exists check: one LDS add per wave
+    const uint32_t c = (uint32_t)__popcll(__ballot(owned_id));
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&aux, c << SHX_OWN_SHIFT);
+  }
   // block sum of the amounts below 2^64: wave sums of the two 64-bit halves, then one LDS word per wave
   const uint64_t a = ((uint64_t)(amount_upper >> 64) != 0) ? 0ull : (uint64_t)amount_upper;
   u128 v = a;
