@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     s.id_ent[i] = id_ent;
     s.pid_ent[i] = pid_ent;
     s.amt[i] = amt;
-    s.pamt[i] = pamt;
+    if (cls & C_POSTVOID) s.pamt[i] = pamt;  // read only for post/void events (k_final)
     s.ins[i] = 0;
   }
   // Window amount bound: block reduction into this block's partial (k_prep_reduce sums them; a
