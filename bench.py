@@ -16,14 +16,16 @@ src/tigerbeetle/benchmark_load.zig:206-327). `--config` selects the other BASELI
 A "step" is one create_transfers batch of the stream, committed through the engine's
 device-resident C ABI in windows of --window consecutive batches (tbg_commit_window: pulse
 decision + pulse, then the batches with their own timestamps and replies, the harness order of
-state_machine.zig:2719-2739). The first W batches are warmup; the next K are timed between
-barrier + stream syncs, max over ranks. `value` counts every committed event (failed ones too:
+state_machine.zig:2719-2739). The whole configured stream is always committed (so the engine's
+state reaches the config's full size): the first W batches (rounded up to whole windows) are
+warmup, and every later batch is timed between barrier + stream syncs, max over ranks; --steps K is
+a minimum, and `steps` reports the timed count. `value` counts every committed event (failed ones too:
 they are committed with a result code); `results.ok_events_per_s` counts the successful ones.
 
 Multi-GPU (torchrun, one rank per GPU): cfg5 shards one global stream over the ranks (accounts and
 transfer ids hash-partitioned, cross-shard facts exchanged by RCCL all-reduce; weak scaling: the
-stream grows with N). cfg1-cfg4 at N > 1 run one independent account shard per rank with its own
-stream (no data-path collective). See DESIGN.md §7.
+stream grows with N). cfg1-cfg4 at N > 1 run N independent databases (one per rank, own stream, no
+data-path collective) and are labelled "replicas", not a scaling run. See DESIGN.md §7.
 
 Extra JSON fields: `roofline` for the dominant kernel (HIP events on the engine stream over the
 timed region) and `cpu_baseline` (the single-threaded C restatement, oracle/, on a bounded prefix
@@ -110,7 +112,9 @@ def parse():
                    help="default: cfg2 on one GPU, cfg5 (sharded) on several")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="process group; gloo lets ranks share one GPU (rehearsal), exchange via host")
-    p.add_argument("--steps", type=int, default=None, help="timed batches (default: rest of the stream)")
+    p.add_argument("--steps", type=int, default=None,
+                   help="minimum timed batches: the whole configured stream is always committed, the first "
+                        "--warmup batches untimed and every later batch timed (so the timed count is >= steps)")
     p.add_argument("--warmup", type=int, default=None, help="warmup batches (rounded to whole windows)")
     p.add_argument("--window", type=int, default=None, help="batches per commit window (super-batching)")
     p.add_argument("--accounts", type=int, default=None)
@@ -167,6 +171,24 @@ class HostStream:
         return self.w.transfers_uniform(first, count, self.seed, a.accounts)
 
 
+def host_cpu():
+    """The host's CPU model and core counts (the baseline names its cores)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+
+
 def cpu_baseline(args, seed):
     """Single-threaded C restatement (oracle/liboracle.so) on a time-bounded prefix of the same
     stream, same harness protocol (pulse when due, then the batch); only the commit calls are
@@ -207,7 +229,7 @@ def cpu_baseline(args, seed):
             events += len(ev)
         first += chunk
     L.tbo_destroy(h)
-    return {
+    line = {
         "value": events / spent,
         "unit": "transfers/s",
         "cores": 1,
@@ -215,6 +237,8 @@ def cpu_baseline(args, seed):
         "sample": f"first {events} transfers of the same {args.config} stream (same accounts and setup), "
                   f"{spent:.1f} s of commit time on 1 host core (oracle/tb_oracle.c, -O2)",
     }
+    line.update(host_cpu())
+    return line
 
 
 # Algorithmic bytes per event of the sharded kernels on one of G shards: every shard
@@ -248,10 +272,11 @@ def run_sharded(args, torch, dist, world, rank, device):
     # N > 1: 128-batch windows (each rank is home for 128 / N of them; rehearsal at G = 8 on one GPU:
     # 5.1G vs 3.3G transfers/s before the collectives, profiles/r1/rehearse_*.json)
     win = max(1, min(args.window if (args.window_set or G == 1) else WINDOW_BATCHES_MAX, WINDOW_BATCHES_MAX))
+    # The whole configured stream is committed (the state always reaches its full size); --warmup
+    # batches are untimed and every later batch is timed (>= --steps of them).
     warm = min(((args.warmup + win - 1) // win) * win, max(0, total_batches - win))
-    steps = args.steps if args.steps is not None else total_batches - warm
-    n_batches = min(total_batches, warm + steps)
-    n_xfer = min(args.transfers * G, n_batches * BATCH)
+    n_batches = total_batches
+    n_xfer = args.transfers * G
     exchange = None if G == 1 else (exchange_gloo if args.backend == "gloo" else exchange_nccl)
     acc_cap = n_acc if G == 1 else int(n_acc / G * 1.02) + 65536
     x_cap = n_xfer if G == 1 else int(n_xfer / G * 1.02) + win * BATCH
@@ -369,6 +394,7 @@ def run_sharded(args, torch, dist, world, rank, device):
             "unit": "transfers/s",
             "n_gpus": world,
             "steps": timed_batches,
+            "steps_requested": args.steps,
             "warmup": warm,
             "ms_per_step": round(elapsed * 1000.0 / timed_batches, 4),
             "higher_is_better": True,
@@ -400,8 +426,27 @@ def run_sharded(args, torch, dist, world, rank, device):
         dist.destroy_process_group()
 
 
+def launch_ranks(args):
+    """`--gpus N` (N > 1) without a launcher: start one rank per GPU the way the driver does (torchrun
+    on 127.0.0.1) as a child process, before anything touches the GPU, and return its exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if world_env is not None and int(world_env) != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s (one rank per GPU)" % (args.gpus, world_env))
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -435,10 +480,11 @@ def main():
     n_setup = n_acc if cfg == "cfg3" else 0
     total_batches = (args.transfers + BATCH - 1) // BATCH
     win = max(1, min(args.window, WINDOW_BATCHES_MAX))
+    # The whole configured stream is committed (the state always reaches its full size); --warmup
+    # batches are untimed and every later batch is timed (>= --steps of them).
     warm = min(((args.warmup + win - 1) // win) * win, max(0, total_batches - win))
-    steps = args.steps if args.steps is not None else total_batches - warm
-    n_batches = min(total_batches, warm + steps)
-    n_xfer = min(args.transfers, n_batches * BATCH)
+    n_batches = total_batches
+    n_xfer = args.transfers
     seed = args.seed + 1000 * rank  # independent stream per shard
 
     sm = StateMachine(device=device, batch_max=BATCH, accounts_max=n_acc_total, transfers_max=n_xfer + n_setup,
@@ -598,16 +644,17 @@ def main():
             "unit": "transfers/s",
             "n_gpus": world,
             "steps": timed_batches,
+            "steps_requested": args.steps,
             "warmup": warm,
             "ms_per_step": round(elapsed * 1000.0 / timed_batches, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if world == 1 else "replicas",
             "vs_baseline": None,
             "dtype": "u128",
             "data": "synthetic (device-generated, seed %d)" % args.seed,
             "config": {"workload": desc, "batch": BATCH, "window_batches": win, "accounts_per_gpu": n_acc,
                        "transfers_per_gpu": n_xfer, "resolver": args.resolver, "change_log": bool(args.change_log),
-                       "parallelism": "independent account shards" if world > 1 else "single GPU"},
+                       "parallelism": "independent databases, one per rank (not sharded)" if world > 1 else "single GPU"},
             "results": {"failed_events_timed": int(all_fails),
                         "ok_events_per_s": round((all_events - all_fails) / elapsed, 1),
                         "walker_events_timed": stats["walker_events"] - walker_before,

@@ -50,6 +50,11 @@
 #ifndef TBG_NT_LOAD
 #define TBG_NT_LOAD 1
 #endif
+// TBG_EXPERIMENTS=1 builds a timing-experiment library (TBG_EXPERIMENT_SKIP switches parts of
+// k_final off; results are then wrong). Release builds compile the switches out.
+#ifndef TBG_EXPERIMENTS
+#define TBG_EXPERIMENTS 0
+#endif
 #ifndef TBG_NT_STORE
 #define TBG_NT_STORE 1
 #endif
@@ -771,7 +776,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
       // side, and a post's posted pair
       Add128 a_dr, a_cr, a_dr2, a_cr2;
       const bool small = d.g->small_win != 0;
-      if (!wev && (cls & C_COMMIT) && !(o.xskip & 1)) {
+      if (!wev && (cls & C_COMMIT) && !(TBG_EXPERIMENTS && (o.xskip & 1))) {
         tb_account_t* dra = &d.acc[s.dr_slot[i]];
         tb_account_t* cra = &d.acc[s.cr_slot[i]];
         const u128 a = s.amt[i];
@@ -805,7 +810,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
           if (cls & C_POSTVOID) rw_post_void(rec, &d.xr[s.p_tslot[i]], s.amt[i]);
         }
         // records of a prefix-extending window are found by binary search (x_prefix_find)
-        if (!(o.xskip & 2) && !prefix_win) x_insert(d.x_tab, d.x_mask, rw_u128(rec[0]), (uint32_t)slot);
+        if (!(TBG_EXPERIMENTS && (o.xskip & 2)) && !prefix_win) x_insert(d.x_tab, d.x_mask, rw_u128(rec[0]), (uint32_t)slot);
         uint8_t st = 0;
         if ((rec[7].y >> 16) & TB_TRANSFER_PENDING) {
           st = wev ? s.bstatus[i] : (uint8_t)TB_PENDING_PENDING;
@@ -850,7 +855,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     for (int q = 0; q < 8; q++) ws[(rins - r0) * 8 + q] = rec[q];
   }
   wave_sync();
-  if (!(o.xskip & 4)) {
+  if (!(TBG_EXPERIMENTS && (o.xskip & 4))) {
     uint4* dst = reinterpret_cast<uint4*>(XFER ? (void*)d.xr : (void*)d.acc) + (size_t)(xbase + r0) * 8;
     for (uint32_t k = lane; k < nins * 8; k += 64) st_stream(dst + k, ws[k]);
   }
