@@ -53,6 +53,8 @@ typedef struct tbg_config {
 #define TBG_E_DEVICE (-3)    /* HIP runtime / device failure: fatal */
 #define TBG_E_STATE (-4)     /* API misuse (e.g. commit timestamp not increasing) */
 #define TBG_E_UNSUPPORTED (-5) /* sharded engine: a window outside the sharded class (nothing applied) */
+#define TBG_E_WINDOW (-6)    /* a commit window spanned a due pulse: it and every window queued after it
+                                were skipped whole (pulse included); resubmit them in smaller windows */
 
 /* StateMachine.init (state_machine.zig:455-477) / deinit (:479-484). */
 int tbg_create(const tbg_config *config, tbg_engine **out);
@@ -61,7 +63,10 @@ int tbg_destroy(tbg_engine *engine);
 /* StateMachine.input_valid (state_machine.zig:543-572). Returns 1 valid, 0 invalid. */
 int tbg_input_valid(const tbg_engine *engine, uint32_t operation, uint64_t input_len);
 
-/* StateMachine.pulse (state_machine.zig:589-596): *needed = pulse_next_timestamp <= prepare_ts. */
+/* StateMachine.pulse (state_machine.zig:589-596): *needed = pulse_next_timestamp <= prepare_ts, with
+ * the reference's exact pulse_next_timestamp (lowered by every timeout creation that ran ok, also in
+ * a chain rolled back later; reset to timestamp_min by a post/void of the transfer whose expiry it
+ * holds; set by each pulse's finish). Synchronizes. */
 int tbg_pulse_needed(tbg_engine *engine, uint64_t prepare_timestamp, int *needed);
 
 /* StateMachine.prefetch (state_machine.zig:598-648): stages the request on the device and resolves
@@ -86,19 +91,26 @@ int tbg_commit_device(tbg_engine *engine, uint32_t operation, uint64_t timestamp
 
 /* Super-batching: commits n_batches consecutive prepared batches (events contiguous in HBM at
  * d_events, batch b has batch_events[b] events and commit timestamp batch_timestamps[b]) in one
- * pass, with results identical to committing them one by one. Replies land in d_results,
- * concatenated per batch: batch b's replies are entries [d_batch_base[b], d_batch_base[b+1]), each
- * with a batch-relative index. Requires that no pulse can fall due between the window's batches
- * (the device checks this; tbg_sync() then fails with TBG_E_STATE). With `auto_pulse`, the pulse
- * decision for the first batch (pulse_next <= prepare_timestamp) and the pulse run first.
- * Asynchronous on the engine stream. n_batches <= 128, total events <= window_events_max. */
+ * pass, with results identical to committing them one by one under the harness protocol (a pulse
+ * check before every batch, state_machine.zig:2719-2739). Replies land in d_results, concatenated
+ * per batch: batch b's replies are entries [d_batch_base[b], d_batch_base[b+1]), each with a
+ * batch-relative index. With `auto_pulse`, the pulse decision for the first batch
+ * (pulse_next <= prepare_timestamp) and the pulse run first, on the device. A pulse that expires
+ * nothing inside the window (after a post/void reset pulse_next) is modelled exactly; a window in
+ * which a pulse with expiries would fall due is rejected whole on the device (nothing applied, its
+ * pulse included, and every window queued after it skipped too): tbg_sync() returns TBG_E_WINDOW
+ * and tbg_windows_committed() tells how many windows were applied. Asynchronous on the engine
+ * stream. n_batches <= 128, total events <= window_events_max. */
 int tbg_commit_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_batches,
                       const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_results,
                       uint32_t *d_batch_base, int auto_pulse, uint64_t prepare_timestamp);
 
-/* Waits for all work queued on the engine's stream; TBG_E_STATE if a submitted window needed a
- * pulse inside it (its results must not be trusted). */
+/* Waits for all work queued on the engine's stream. TBG_E_WINDOW (reported once) if a window was
+ * rejected (see tbg_commit_window). */
 int tbg_sync(tbg_engine *engine);
+/* Create_* windows (and single-batch commits) applied by the device, and submitted by the host,
+ * since tbg_create: after TBG_E_WINDOW, windows [applied, submitted) changed nothing. Synchronizes. */
+int tbg_windows_committed(tbg_engine *engine, uint64_t *applied, uint64_t *submitted);
 /* The engine's HIP stream (hipStream_t), for callers that time or order around it. */
 void *tbg_stream(tbg_engine *engine);
 

@@ -40,6 +40,8 @@ def _chaos_run(seed, batches, batch_max, tick_every=3, **kw):
             r1 = run_protocol(gpu, op, ev, tick)
             r2 = run_protocol(ref, op, ev, tick)
             assert r1 == r2, f"seed {seed} batch {b}: gpu {np.frombuffer(r1, '<u4')} ref {np.frombuffer(r2, '<u4')}"
+            # the next pulse() decision (state_machine.zig:589-596) reads this value
+            assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp(), f"seed {seed} batch {b}"
         _compare_final(gpu, ref)
         return gpu.stats()
     finally:

@@ -17,7 +17,7 @@ EXPORTS = [
     "tbg_timing_enable", "tbg_timing_collect", "tbg_gen_accounts_cfg3", "tbg_gen_funding_cfg3",
     "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4", "tbg_debug_counters", "tbg_shard_of",
     "tbg_shard_prepare_window", "tbg_shard_decide_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
-    "tbg_shard_commit_bits_bytes", "tbg_window_changes",
+    "tbg_shard_commit_bits_bytes", "tbg_window_changes", "tbg_windows_committed",
 ]
 
 
@@ -104,6 +104,7 @@ def lib():
         "tbg_shard_commit_bits_bytes": ([u32], u64),
         "tbg_window_changes": ([vp, vp, u64, P(u64), vp, u64, P(u64), vp, u64, P(u64)], i32),
         "tbg_shard_exchange_bytes": ([u32, u32], u64),
+        "tbg_windows_committed": ([vp, P(u64), P(u64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -114,14 +115,22 @@ def lib():
 
 
 E_UNSUPPORTED = -5
+E_WINDOW = -6
 
 
 class UnsupportedWindow(RuntimeError):
     """A sharded engine rejected a window outside its class (nothing was applied)."""
 
 
+class RejectedWindow(RuntimeError):
+    """A commit window spanned a due pulse: it and every window queued after it were skipped whole
+    (tbg_commit_window); resubmit them in smaller windows."""
+
+
 def check(rc, what):
     if rc == E_UNSUPPORTED:
         raise UnsupportedWindow(f"{what}: window outside the sharded class (status {rc})")
+    if rc == E_WINDOW:
+        raise RejectedWindow(f"{what}: a window spanned a due pulse and was skipped whole (status {rc})")
     if rc != 0:
         raise RuntimeError(f"{what} failed with status {rc}")

@@ -9,7 +9,7 @@
 //     (k_chg_mark; plain stores, every writer stores the same value), then listed in slot order
 //     (k_chg_count, k_chg_scan, k_chg_list);
 //   - earlier pending transfers that a committed post/void resolved are listed by k_chg_mark.
-// k_pulse_apply marks the accounts and lists the transfers of every expiry the same way. A commit
+// k_pulse_tail marks the accounts and lists the transfers of every expiry the same way. A commit
 // call's log covers its pulse (if any) and its window. tbg_window_changes gathers and copies them.
 #pragma once
 #include "window.h"
@@ -25,9 +25,9 @@ struct ChgLog {
 };
 
 template <bool XFER>
-__global__ void __launch_bounds__(256) k_chg_mark(Scratch s, uint32_t E, uint32_t epoch, ChgLog c) {
+__global__ void __launch_bounds__(256) k_chg_mark(Scratch s, const Globals* g, uint32_t E, uint32_t epoch, ChgLog c) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E || s.code[i] != TB_CT_OK) return;
+  if (i >= E || WIN_REJECTED(g) || s.code[i] != TB_CT_OK) return;
   if (!XFER) return;  // new accounts are the store slice
   const uint32_t dr = s.dr_slot[i], cr = s.cr_slot[i];
   // a post/void of a pending transfer created in this window may carry no slots: its creator,

@@ -17,7 +17,9 @@
 #pragma once
 #include "walker.h"
 
-__device__ inline bool cpw_active(const Globals* g) { return !g->hot_count && !window_ovf_mode(g); }
+__device__ inline bool cpw_active(const Globals* g) {
+  return !WIN_REJECTED(g) && !g->hot_count && !window_ovf_mode(g);
+}
 
 __device__ inline uint32_t cc_find(const uint32_t* parent, uint32_t x) {
   for (;;) {

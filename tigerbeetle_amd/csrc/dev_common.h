@@ -69,7 +69,7 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t acc_count;
   uint64_t x_count;
   uint64_t exp_count;
-  uint64_t pulse_next;  // ExpirePendingTransfers.pulse_next_timestamp (conservative)
+  uint64_t pulse_next;  // ExpirePendingTransfers.pulse_next_timestamp, exact (k_pn)
   u128 ovf_bound;       // >= every account's dp+dpo and cp+cpo (overflow-free batch test)
   // per batch
   u128 batch_amount_sum;
@@ -78,7 +78,10 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t result_count;
   uint32_t insert_count;
   uint32_t w_count;
-  uint32_t window_error;  // a multi-batch window was submitted although a pulse could fall due inside
+  // bit 0: a window was rejected whole because a pulse with expiries would fall due inside it
+  // (sticky: every later window is skipped until tbg_sync reports and clears it); bit 1: sharded
+  // window outside the class; bit 2: index guard
+  uint32_t window_error;
   uint64_t base;  // acc_count / x_count at batch start (captured by the scan kernel)
   // pulse
   uint32_t cand_count;
@@ -117,7 +120,12 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t mono_prev;   // the previous transfer window was claim-free (k_ct_prep's speculation)
   uint64_t x_id_max;    // >= every stored transfer id (u64 max once any id needs > 64 bits): an id
                         // above it cannot exist, so its table probe is skipped (monotonic ids)
+  uint64_t windows_applied;  // create_* windows applied (rejected windows excluded), cumulative
 };
+
+// A rejected window (Globals::window_error bit 0) is skipped by every kernel that could change
+// state, and so is every window queued after it, until the host has seen the error (tbg_sync).
+#define WIN_REJECTED(g) (__builtin_expect(((g)->window_error & 1u) != 0, 0))
 
 // Per-event class bits (scratch `cls`).
 enum : uint32_t {
@@ -140,6 +148,10 @@ enum : uint32_t {
   C_RES_DR = 1u << 16,     // final: the resolver applied this event's debit-account effects
   C_RES_CR = 1u << 17,     // final: the resolver applied this event's credit-account effects
   C_OWN = 1u << 18,        // sharded: this shard owns the event's id (it inserts the record)
+  C_PNOP = 1u << 19,       // pulse_next op candidate (scratch pnv): a pending create with a timeout, or
+                           // a post/void of a pending transfer with a timeout (state_machine.zig:1576-1581,
+                           // 1704-1708); applies if the event ran ok, even if its chain is rolled back
+  C_RANOK = 1u << 20,      // ran ok, then rolled back with its chain (code back-filled linked_event_failed)
 };
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

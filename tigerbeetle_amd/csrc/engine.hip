@@ -91,15 +91,6 @@ __device__ inline uint32_t acc_probe_from(const AccEntry* __restrict__ tab, uint
   }
 }
 
-// A window may hold several batches only if no pulse can fall due inside it: live expiry entries
-// are >= pulse_next, and entries created inside the window expire >= its first timestamp + 1 s.
-__device__ inline void check_window(const WinDesc& w, Globals* g) {
-  if (w.nb <= 1) return;
-  const uint64_t last = w.T[w.nb - 1];
-  const uint64_t first_ts = win_ts(w, 0, w.off[0]);
-  if (last >= g->pulse_next || last >= first_ts + TB_NS_PER_S) g->window_error = 1;
-}
-
 // A balance-reading decision makes the read account hot for this window: every event touching it
 // is then decided in order (resolver.h or the walker). The first marker assigns the account its
 // dense rank (one counter atomic per wave).
@@ -123,10 +114,11 @@ __device__ inline void mark_hot(Dev d, uint32_t slot, uint32_t epoch) {
 __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
                                                  uint32_t epoch) {
   __shared__ u128 red[256];
-  __shared__ uint32_t aux;  // bit 0 huge amount, bit 1 not claim-free, bit 2 first id above every stored id
+  // bit 0 huge amount, bit 1 not claim-free, bit 2 first id above every stored id, bit 3 pulse_next op
+  __shared__ uint32_t aux;
+  if (WIN_REJECTED(d.g)) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (threadIdx.x == 0) aux = 0;
-  if (i == 0) check_window(w, d.g);
   __syncthreads();
   u128 amount_upper = 0;
   if (i < w.E) {
@@ -148,6 +140,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     uint32_t dr_slot = NONE32, cr_slot = NONE32, id_tslot = NONE32, p_tslot = NONE32, id_ent = NONE32,
              pid_ent = NONE32;
     u128 amt = 0, pamt = 0;
+    uint64_t pnv = 0;
     const uint16_t f = t.flags;
     if (f & TB_TRANSFER_LINKED) cls |= C_LINKED;
     if (t.timestamp != 0) {
@@ -183,6 +176,11 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
           } else {
             cls |= C_PV_PREBATCH;
             const tb_transfer_t p = d.xr[p_tslot];
+            if ((p.flags & TB_TRANSFER_PENDING) && p.timeout > 0) {
+              // if it runs ok, it removes p's expires_at entry and may reset pulse_next (:1698-1708)
+              pnv = expires_at_of(p);
+              cls |= C_PNOP;
+            }
             code = pv_against(t, p, &amt);
             if (p.flags & TB_TRANSFER_PENDING) {
               AccEntry de, ce;
@@ -249,6 +247,11 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
               } else {
                 code = TB_CT_OK;
                 cls |= C_INSERT;
+                if ((f & TB_TRANSFER_PENDING) && t.timeout > 0) {
+                  // if it runs ok, pulse_next = min(pulse_next, expires_at) (:1576-1581)
+                  pnv = t.timestamp + (uint64_t)t.timeout * TB_NS_PER_S;
+                  cls |= C_PNOP;
+                }
               }
             }
           }
@@ -256,6 +259,10 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
       }
     }
     if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&aux, 1u);
+    if (cls & C_PNOP) {
+      s.pnv[i] = pnv;
+      atomicOr(&aux, 8u);
+    }
     // Hot marks: the first marker of an account this window gives it the next dense rank.
     if (cls & C_READS_DR) mark_hot(d, dr_slot, epoch);
     if (cls & C_READS_CR) mark_hot(d, cr_slot, epoch);
@@ -301,6 +308,7 @@ __device__ inline u128 block_sum_u128(u128 v, u128* lds) {
 __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t nblk) {
   __shared__ u128 red[1024];
   __shared__ uint32_t aux;
+  if (WIN_REJECTED(d.g)) return;
   if (threadIdx.x == 0) aux = 0;
   __syncthreads();
   u128 v = 0;
@@ -317,7 +325,7 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
     if (aux & 1u) g->batch_huge = 1;
     const bool claim_free = !(aux & 2u);
     const bool prefix = claim_free && (aux & 4u) && g->x_sorted == g->x_count;
-    g->win_flags = (claim_free ? 1u : 0u) | (prefix ? 2u : 0u);
+    g->win_flags = (claim_free ? 1u : 0u) | (prefix ? 2u : 0u) | ((aux & 8u) ? 4u : 0u);
     // every balance field stays below 2^64 this window (k_walk computes the same for k_final; the
     // component walkers, which run before k_walk, read it from here)
     const u128 sum = g->ovf_bound + g->batch_amount_sum;
@@ -329,7 +337,7 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
 // that is not gets its key-map claims here, before anything reads the map.
 __global__ void __launch_bounds__(256) k_claim_fix(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, uint32_t E,
                                                    uint32_t epoch) {
-  if (!d.g->mono_prev || (d.g->win_flags & 1u)) return;
+  if (WIN_REJECTED(d.g) || !d.g->mono_prev || (d.g->win_flags & 1u)) return;
   // grid-stride over a capped grid: the common case (speculation right) is a launch whose blocks
   // exit at once, so it pays for few blocks
   const uint8_t* evb = reinterpret_cast<const uint8_t*>(ev);
@@ -356,8 +364,7 @@ __device__ inline bool window_ovf_mode(const Globals* g) {
 __global__ void __launch_bounds__(256) k_ca_prep(Dev d, Scratch s, const tb_account_t* __restrict__ ev, WinDesc w,
                                                  uint32_t epoch) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) check_window(w, d.g);
-  if (i >= w.E) return;
+  if (i >= w.E || WIN_REJECTED(d.g)) return;
   const tb_account_t a = ev[i];
   const uint32_t b = win_batch(w, i);
   uint32_t cls = 0, code, id_ent = NONE32, slot = NONE32;
@@ -480,13 +487,16 @@ __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinD
       code = TB_CT_LINKED_EVENT_FAILED;
     const bool commit = f == NONE32;
     s.code[j] = code;
-    s.cls[j] = cj | (commit ? C_COMMIT : 0) | ((commit && (cj & C_INSERT)) ? C_INSERTED : 0);
+    // members before the first failure ran ok before the rollback (their pulse_next ops stand)
+    const uint32_t ranok = (f != NONE32 && j < f) ? C_RANOK : 0u;
+    s.cls[j] = cj | ranok | (commit ? C_COMMIT : 0) | ((commit && (cj & C_INSERT)) ? C_INSERTED : 0);
   }
   return any_w;  // a chain in W: walker
 }
 
 template <bool XFER>
 __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, uint32_t epoch) {
+  if (WIN_REJECTED(d.g)) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool ovf_mode = XFER && window_ovf_mode(d.g);
   bool bad = false;
@@ -553,6 +563,7 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
                                                         uint32_t nseg, uint32_t epoch) {
   __shared__ uint32_t lds[WALK_THREADS / 64];
   __shared__ uint32_t sbad[MAX_SEGS], sins[MAX_SEGS];
+  if (WIN_REJECTED(d.g)) return;
   if (threadIdx.x == 0) {
     Globals* g = d.g;
     g->base = XFER ? g->x_count : g->acc_count;
@@ -709,6 +720,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   __shared__ uint32_t lds[SEG / 64];
   __shared__ unsigned long long ldsm[SEG / 64];
   __shared__ uint4 stage[SEG * 8];  // one 128 B record per event: 128 KiB
+  if (WIN_REJECTED(d.g)) return;
   unsigned long long id_key = 0;  // this thread's inserted transfer id, for Globals::x_id_max
   const bool prefix_win = XFER && (d.g->win_flags & 2u) != 0;  // k_prep_reduce
   const uint32_t E = w.E;
@@ -818,7 +830,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
           if (timeout > 0) {
             const uint64_t ts = rw_u64(rec[7].z, rec[7].w);
             const uint64_t expires_at = ts + (uint64_t)timeout * TB_NS_PER_S;  // expires_at_of
-            atomicMin(reinterpret_cast<unsigned long long*>(&d.g->pulse_next), (unsigned long long)expires_at);
+            // (pulse_next is k_pn's: it also counts creations that a failing chain rolled back)
             const bool visible = !(ts >> 63) && expires_at <= TB_TIMESTAMP_MAX;
             if (st == TB_PENDING_PENDING && visible) {
               const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), 1ull);
@@ -877,6 +889,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     } else {
       gw->acc_count = xbase + total_ins;
     }
+    gw->windows_applied++;
     gw->hot_count = 0;
     gw->res_inelig = 0;
     gw->res_error = 0;
@@ -885,6 +898,173 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     gw->light_count = 0;
     gw->cpw_done = 0;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// pulse_next_timestamp, exact (state_machine.zig:1576-1581, 1704-1708, 2112-2145). The reference
+// keeps it outside every groove, so a chain rollback undoes none of its edits:
+//   - every create_transfer that runs ok with a timeout lowers it to its expires_at (:1576-1581);
+//   - every post/void that runs ok on a pending transfer with a timeout resets it to timestamp_min
+//     when it equals that transfer's expires_at (:1704-1708).
+// Once reset, it stays timestamp_min until the next batch's pulse check (the harness pulses before
+// every batch, :2719-2739), where the pulse expires nothing (the window check guarantees it) and
+// its finish sets the first live expires_at or timestamp_max (:2126-2135). k_pn replays exactly
+// that over the window's ops in event order; events that ran ok are the committed ones plus the
+// rolled-back chain members marked C_RANOK.
+// ------------------------------------------------------------------------------------------------
+// The event's op: 0 none, 1 creation (value x), 2 reset candidate (value y).
+__device__ inline uint32_t pn_op(const Scratch& s, uint32_t i, uint64_t* v) {
+  const uint32_t cls = s.cls[i];
+  if (!(cls & C_PNOP)) return 0;
+  if (s.code[i] != TB_CT_OK && !(cls & C_RANOK)) return 0;
+  *v = s.pnv[i];
+  return (cls & C_POSTVOID) ? 2u : 1u;
+}
+
+__device__ inline unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
+
+// Block-wide minimum of a u64 (one LDS word per wave), result valid in every thread.
+template <int NWAVES>
+__device__ inline unsigned long long block_min_u64(unsigned long long v, unsigned long long* lds) {
+  return ~block_max_u64<NWAVES>(~v, lds);
+}
+
+// Exclusive prefix minimum over the block's threads (identity ~0); *total = the block minimum.
+template <int NWAVES>
+__device__ inline unsigned long long block_excl_min_u64(unsigned long long v, unsigned long long* lds,
+                                                        unsigned long long* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc = umin64(inc, y);
+  }
+  unsigned long long ex = __shfl_up(inc, 1, 64);
+  if (lane == 0) ex = ~0ull;
+  if (lane == 63) lds[wave] = inc;
+  __syncthreads();
+  unsigned long long wp = ~0ull, tot = ~0ull;
+#pragma unroll
+  for (int k = 0; k < NWAVES; k++) {
+    const unsigned long long x = lds[k];
+    if (k < wave) wp = umin64(wp, x);
+    tot = umin64(tot, x);
+  }
+  __syncthreads();
+  *total = tot;
+  return umin64(wp, ex);
+}
+
+// Per segment: the minimum creation value and the number of reset candidates, over the events
+// that ran ok. Only windows whose prep saw a candidate (win_flags bit 2) do any work.
+__global__ void __launch_bounds__(SEG) k_pn_seg(Dev d, Scratch s, uint32_t E) {
+  __shared__ uint32_t lds[SEG / 64];
+  __shared__ unsigned long long ldsm[SEG / 64];
+  if (WIN_REJECTED(d.g) || !(d.g->win_flags & 4u)) return;
+  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
+  unsigned long long x = ~0ull;
+  uint32_t r = 0;
+  if (i < E) {
+    uint64_t v = 0;
+    const uint32_t op = pn_op(s, i, &v);
+    if (op == 1) x = v;
+    if (op == 2) r = 1;
+  }
+  const unsigned long long m = block_min_u64<SEG / 64>(x, ldsm);
+  const uint32_t n = block_sum<SEG / 64>(r, lds);
+  if (threadIdx.x == 0) {
+    s.pn_min[blockIdx.x] = m;
+    s.pn_res[blockIdx.x] = n;
+  }
+}
+
+#define PN_THREADS 1024
+
+// The pulse at the start of batch b >= 1 after a reset: nothing is due (window check), so its
+// finish sets the minimum expires_at among the entries live at that point, else timestamp_max.
+// Live then = (A) entries pending now and created before batch b (pre-window slots, or records
+// stamped <= T_{b-1}), plus (B) pending transfers that a committed post/void of batch >= b removed,
+// created before batch b. Rare (a reset inside a multi-batch window): one workgroup, plain loops.
+__device__ uint64_t pn_minlive(const Dev& d, const Scratch& s, const WinDesc& w, uint32_t b,
+                               unsigned long long* ldsm) {
+  const uint64_t base = d.g->base;
+  const uint64_t t_prev = w.T[b - 1];
+  unsigned long long m = ~0ull;
+  const ExpEntry* list = d.exp[*d.exp_cur];
+  const uint64_t cnt = d.g->exp_count;
+  for (uint64_t j = threadIdx.x; j < cnt; j += PN_THREADS) {
+    const ExpEntry e = list[j];
+    if (d.xstatus[e.slot] != TB_PENDING_PENDING) continue;
+    if (e.slot >= base && d.xr[e.slot].timestamp > t_prev) continue;  // created in batch >= b
+    m = umin64(m, e.expires_at);
+  }
+  for (uint32_t k = w.off[b] + threadIdx.x; k < w.E; k += PN_THREADS) {
+    const uint32_t cls = s.cls[k];
+    if (!(cls & C_POSTVOID) || !(cls & C_PNOP) || s.code[k] != TB_CT_OK) continue;
+    uint64_t pts;
+    const uint32_t ps = s.p_tslot[k];
+    if (ps != NONE32) {
+      pts = d.xr[ps].timestamp;  // created before the window
+    } else {
+      const uint32_t pc = s.pn_src[k];
+      if (s.batch[pc] >= b) continue;
+      pts = win_ts(w, s.batch[pc], pc);
+    }
+    const uint64_t y = s.pnv[k];
+    if ((pts >> 63) || y > TB_TIMESTAMP_MAX) continue;  // never visible to the scan (composite key)
+    m = umin64(m, y);
+  }
+  m = block_min_u64<PN_THREADS / 64>(m, ldsm);
+  return m == ~0ull ? TB_TIMESTAMP_MAX : m;
+}
+
+__global__ void __launch_bounds__(PN_THREADS) k_pn(Dev d, Scratch s, WinDesc w) {
+  __shared__ unsigned long long ldsm[PN_THREADS / 64];
+  __shared__ uint32_t first_eff, next_seg;
+  if (WIN_REJECTED(d.g) || !(d.g->win_flags & 4u)) return;
+  const uint32_t E = w.E, nseg = (E + SEG - 1) / SEG;
+  uint64_t pn = d.g->pulse_next;  // after the pulse before the window
+  uint32_t i = 0;
+  while (i < E) {
+    if (i % SEG == 0) {
+      // fold whole segments without a reset candidate; stop at the next one that has some
+      const uint32_t s0 = i / SEG;
+      if (threadIdx.x == 0) next_seg = NONE32;
+      __syncthreads();
+      for (uint32_t j = s0 + threadIdx.x; j < nseg; j += PN_THREADS)
+        if (s.pn_res[j]) atomicMin(&next_seg, j);
+      __syncthreads();
+      const uint32_t stop = next_seg == NONE32 ? nseg : next_seg;
+      unsigned long long m = ~0ull;
+      for (uint32_t j = s0 + threadIdx.x; j < stop; j += PN_THREADS) m = umin64(m, s.pn_min[j]);
+      pn = umin64(pn, block_min_u64<PN_THREADS / 64>(m, ldsm));
+      if (stop == nseg) break;
+      i = stop * SEG;
+    }
+    // event by event, within one segment and one batch
+    const uint32_t b = s.batch[i];
+    const uint32_t end = min(min((i / SEG + 1) * SEG, E), w.off[b + 1]);
+    const uint32_t k = i + threadIdx.x;
+    uint64_t v = 0;
+    const uint32_t op = k < end ? pn_op(s, k, &v) : 0u;
+    unsigned long long tot;
+    const unsigned long long before = umin64(pn, block_excl_min_u64<PN_THREADS / 64>(op == 1 ? v : ~0ull, ldsm, &tot));
+    if (threadIdx.x == 0) first_eff = NONE32;
+    __syncthreads();
+    if (op == 2 && before == v) atomicMin(&first_eff, k);
+    __syncthreads();
+    if (first_eff != NONE32) {
+      // reset to timestamp_min (:1706-1707); the next batch's pulse finds nothing due
+      i = w.off[b + 1];
+      pn = b + 1 < w.nb ? pn_minlive(d, s, w, b + 1, ldsm) : TB_TIMESTAMP_MIN;
+    } else {
+      pn = umin64(pn, tot);
+      i = end;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) d.g->pulse_next = pn;
 }
 
 #include "shard.h"
@@ -896,21 +1076,41 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
 // ------------------------------------------------------------------------------------------------
 struct PulseCtl {
   uint32_t active;
-  uint32_t select_all;
-  uint64_t thr_expires_at;  // selection threshold key (expires_at, slot), inclusive
-  uint32_t thr_slot;
   uint32_t pad;
 };
 
-__global__ void k_pulse_gate(Dev d, PulseCtl* ctl, uint64_t prepare_timestamp) {
-  ctl->active = d.g->pulse_next <= prepare_timestamp ? 1u : 0u;  // pulse() (:589-596)
-  d.g->cand_count = 0;
-  d.g->alt_count = 0;
-  d.g->next_min = ~0ull;
+// The window a pulse decision precedes: a window of several batches is valid only if no pulse can
+// fall due inside it (the harness runs a pulse check before every batch, state_machine.zig:
+// 2719-2739). Live expires_at entries are >= pulse_next (an invariant of the reference value too:
+// finish sets it to the first live entry past the scan, creations only lower it, and a post/void
+// reset only lowers it); entries the window creates expire >= its first timestamp + 1 s.
+struct WinChk {
+  uint32_t nb;
+  uint64_t T_last, first_ts;
+};
+__device__ inline bool window_spans_pulse(const WinChk& c, uint64_t pulse_next) {
+  return c.nb > 1 && (c.T_last >= pulse_next || c.T_last >= c.first_ts + TB_NS_PER_S);
 }
 
-__global__ void __launch_bounds__(256) k_pulse_scan(Dev d, Scratch s, const PulseCtl* ctl, uint64_t T) {
-  if (!ctl->active) return;
+// pulse() (:589-596) and the expires_at scan (:1010-1043, value_next :2147-2166): the due live
+// entries go to `cand`, the others to the alternate list. When no pulse runs, block 0 checks the
+// window against the current pulse_next; a window that spans a due pulse is rejected whole
+// (window_error bit 0): it and every window after it change nothing until tbg_sync reports it.
+// Counters (cand_count, alt_count, next_min) are zero here: k_pulse_tail leaves them so.
+__global__ void __launch_bounds__(256) k_pulse_scan(Dev d, Scratch s, PulseCtl* ctl, uint64_t T,
+                                                    uint64_t prepare_timestamp, WinChk chk) {
+  const bool first = blockIdx.x == 0 && threadIdx.x == 0;
+  if (WIN_REJECTED(d.g)) {
+    if (first) ctl->active = 0;
+    return;
+  }
+  const uint64_t pn = d.g->pulse_next;
+  const bool active = pn <= prepare_timestamp;
+  if (first) {
+    ctl->active = active ? 1u : 0u;
+    if (!active && window_spans_pulse(chk, pn)) atomicOr(&d.g->window_error, 1u);
+  }
+  if (!active) return;
   const uint32_t cur = *d.exp_cur;
   const ExpEntry* list = d.exp[cur];
   ExpEntry* alt = d.exp[cur ^ 1];
@@ -929,31 +1129,29 @@ __global__ void __launch_bounds__(256) k_pulse_scan(Dev d, Scratch s, const Puls
   }
 }
 
-// Selection of the `cap` smallest (expires_at, slot) keys: 12-pass LDS radix select (8-bit digits
-// over the 96-bit key), single workgroup. Only runs when more than `cap` transfers are due.
-__global__ void __launch_bounds__(1024) k_pulse_select(Dev d, Scratch s, PulseCtl* ctl, uint32_t cap) {
+// One workgroup: selection of the `cap` smallest (expires_at, slot) keys when more are due (12-pass
+// LDS radix select, 8-bit digits over the 96-bit key; slot order = timestamp order), the finish
+// (:2112-2145) into pulse_next, the window check against that new value, then
+// execute_expire_pending_transfers (:1874-1929) and the list swap. A rejected window leaves
+// everything as it was: the scan only read the live list.
+__global__ void __launch_bounds__(1024) k_pulse_tail(Dev d, Scratch s, PulseCtl* ctl, uint32_t cap, ChgLog chg,
+                                                    uint32_t chg_epoch, WinChk chk) {
   __shared__ uint32_t hist[256];
   __shared__ uint64_t prefix_hi;
   __shared__ uint32_t prefix_lo;
   __shared__ uint32_t want;
+  __shared__ uint32_t reject;
   if (!ctl->active) return;
-  const uint32_t m = d.g->cand_count;
-  if (m <= cap) {
-    if (threadIdx.x == 0) {
-      ctl->select_all = 1;
-      // scan_finished: next = first live entry beyond T, else timestamp_max (:2126-2135)
-      d.g->pulse_next = d.g->alt_count > 0 ? d.g->next_min : TB_TIMESTAMP_MAX;
-      d.g->expired_count = m;
-    }
-    return;
-  }
+  Globals* g = d.g;
+  const uint32_t m = g->cand_count;
+  const bool select_all = m <= cap;
   if (threadIdx.x == 0) {
     prefix_hi = 0;
     prefix_lo = 0;
     want = cap;  // 1-based rank of the last selected key
   }
   __syncthreads();
-  for (int pass = 0; pass < 12; pass++) {
+  for (int pass = 0; !select_all && pass < 12; pass++) {
     const int shift = 88 - 8 * pass;  // bit position of this digit in the 96-bit key
     for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0;
     __syncthreads();
@@ -988,27 +1186,31 @@ __global__ void __launch_bounds__(1024) k_pulse_select(Dev d, Scratch s, PulseCt
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    ctl->select_all = 0;
-    ctl->thr_expires_at = prefix_hi;
-    ctl->thr_slot = prefix_lo;
-    d.g->pulse_next = prefix_hi;  // buffer_finished: last included expires_at (:2136-2140)
-    d.g->expired_count = cap;
+  // finish: scan_finished -> the first live entry beyond T, else timestamp_max; buffer_finished ->
+  // the last included expires_at (another pulse follows)
+  const uint64_t pn_after =
+      select_all ? (g->alt_count > 0 ? g->next_min : TB_TIMESTAMP_MAX) : prefix_hi;
+  const uint64_t thr_e = prefix_hi;
+  const uint32_t thr_s = prefix_lo;
+  if (threadIdx.x == 0) reject = window_spans_pulse(chk, pn_after) ? 1u : 0u;
+  __syncthreads();
+  if (reject) {
+    if (threadIdx.x == 0) {
+      atomicOr(&g->window_error, 1u);
+      g->cand_count = 0;
+      g->alt_count = 0;
+      g->next_min = ~0ull;
+      ctl->active = 0;
+    }
+    return;
   }
-}
-
-__global__ void __launch_bounds__(256) k_pulse_apply(Dev d, Scratch s, const PulseCtl* ctl, ChgLog chg,
-                                                     uint32_t chg_epoch) {
-  if (!ctl->active) return;
-  const uint32_t m = d.g->cand_count;
   const uint32_t cur = *d.exp_cur;
   ExpEntry* alt = d.exp[cur ^ 1];
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+  for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
     const ExpEntry e = s.cand[j];
-    const bool take = ctl->select_all || e.expires_at < ctl->thr_expires_at ||
-                      (e.expires_at == ctl->thr_expires_at && e.slot <= ctl->thr_slot);
+    const bool take = select_all || e.expires_at < thr_e || (e.expires_at == thr_e && e.slot <= thr_s);
     if (!take) {
-      const uint32_t k = atomicAdd(&d.g->alt_count, 1u);
+      const uint32_t k = atomicAdd(&g->alt_count, 1u);
       alt[k] = e;
       continue;
     }
@@ -1026,13 +1228,17 @@ __global__ void __launch_bounds__(256) k_pulse_apply(Dev d, Scratch s, const Pul
       chg.pend[atomicAdd(&chg.cnt[1], 1u)] = e.slot;
     }
   }
-}
-
-__global__ void k_pulse_finish(Dev d, PulseCtl* ctl) {
-  if (!ctl->active) return;
-  *d.exp_cur ^= 1u;
-  d.g->exp_count = d.g->alt_count;
-  ctl->active = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *d.exp_cur = cur ^ 1u;
+    g->exp_count = g->alt_count;
+    g->pulse_next = pn_after;
+    g->expired_count = select_all ? m : cap;
+    g->cand_count = 0;
+    g->alt_count = 0;
+    g->next_min = ~0ull;
+    ctl->active = 0;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------

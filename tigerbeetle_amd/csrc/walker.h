@@ -216,6 +216,13 @@ struct Walker {
     if (r != CONT) return r;
     commit_record(i, pv_record(t, p, amount));
     if (p.timeout > 0 && expires_at_of(p) <= t.timestamp) return TB_CT_PENDING_TRANSFER_EXPIRED;
+    if (pc >= 0 && p.timeout > 0) {
+      // p was created in this window (k_ct_prep could not see it): the expires_at removal and the
+      // pulse_next reset candidate (:1698-1708) for k_pn
+      s.pnv[i] = expires_at_of(p);
+      s.pn_src[i] = (uint32_t)pc;
+      s.cls[i] |= C_PNOP;
+    }
     const uint8_t st = (t.flags & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
     if (pc >= 0) {
       log_small(UNDO_BST, (uint32_t)pc, s.bstatus[pc]);
@@ -295,7 +302,10 @@ struct Walker {
       if (r != TB_CT_OK && chain >= 0 && !broken) {
         broken = true;
         rollback();
-        for (uint32_t j = (uint32_t)chain; j < i; j++) s.code[j] = TB_CT_LINKED_EVENT_FAILED;
+        for (uint32_t j = (uint32_t)chain; j < i; j++) {
+          s.code[j] = TB_CT_LINKED_EVENT_FAILED;
+          s.cls[j] |= C_RANOK;  // ran ok before the rollback: its pulse_next op stands (k_pn)
+        }
       }
       s.code[i] = r;
       if (chain >= 0 && (!linked || r == TB_CT_LINKED_EVENT_CHAIN_OPEN)) {

@@ -81,6 +81,13 @@ struct Scratch {
   uint2* rlink;                               // relax.h: per sorted entry: other side's entry and rank
   uint32_t *heavy, *light;                    // hot ranks by walker kind
   uint32_t *cc_parent, *cc_list;              // component-parallel walker (cpw.h)
+  // pulse_next (k_pn): per event the op's value (C_PNOP) and, for a walker post/void of a pending
+  // transfer created in the window, that transfer's event index; per segment the min creation value
+  // and the count of resets among the events that ran ok
+  uint64_t* pnv;
+  uint32_t* pn_src;
+  uint64_t* pn_min;
+  uint32_t* pn_res;
   void* sort_tmp;
   size_t sort_tmp_bytes;
 };

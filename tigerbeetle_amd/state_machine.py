@@ -159,3 +159,9 @@ class StateMachine:
 
     def sync(self):
         _lib.check(_lib.lib().tbg_sync(self.h), "sync")
+
+    def windows_committed(self):
+        """(applied, submitted) create_* windows since creation (tbg_windows_committed)."""
+        a, s = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(_lib.lib().tbg_windows_committed(self.h, ctypes.byref(a), ctypes.byref(s)), "windows_committed")
+        return a.value, s.value
