@@ -60,7 +60,9 @@ typedef struct tbg_config {
 int tbg_create(const tbg_config *config, tbg_engine **out);
 int tbg_destroy(tbg_engine *engine);
 
-/* StateMachine.input_valid (state_machine.zig:543-572). Returns 1 valid, 0 invalid. */
+/* StateMachine.input_valid (state_machine.zig:543-572), a static function in the reference
+ * (replica.zig:4855 calls StateMachine.input_valid(operation, body)): `engine` may be NULL, which
+ * means batch_max = 8190. Returns 1 valid, 0 invalid. */
 int tbg_input_valid(const tbg_engine *engine, uint32_t operation, uint64_t input_len);
 
 /* StateMachine.pulse (state_machine.zig:589-596): *needed = pulse_next_timestamp <= prepare_ts, with
@@ -143,6 +145,28 @@ int tbg_shard_prepare_window(tbg_engine *engine, uint32_t operation, const void 
 int tbg_shard_decide_window(tbg_engine *engine, const void *d_exchange, uint32_t home_first, uint32_t home_count,
                             void *d_results, uint32_t *d_batch_base, void *d_commit_bits);
 int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, const void *d_commit_bits);
+
+/* StateMachine.open (state_machine.zig:527-541), after a restart or a state sync: an empty engine
+ * takes the LSM forest's objects: every Account and every Transfer in timestamp order (the grooves'
+ * object trees are keyed by timestamp) and, per transfer, its TransferPending status (0 none,
+ * 1 pending, 2 posted, 3 voided, 4 expired; NULL = all 0). pulse_next_timestamp starts at
+ * timestamp_min, as in a freshly initialised StateMachine (:2063). TBG_E_STATE if not empty. */
+int tbg_open(tbg_engine *engine, const tb_account_t *accounts, uint64_t n_accounts, const tb_transfer_t *transfers,
+             uint64_t n_transfers, const uint8_t *pending_status);
+/* StateMachine.reset (state_machine.zig:486-501): back to an empty state machine. */
+int tbg_reset(tbg_engine *engine);
+/* Prefetch completion (state_machine.zig:598-648 completes through a callback, possibly on the next
+ * tick, groove.zig:753-757): *done = 1 once the device work of the last tbg_prefetch finished. */
+int tbg_prefetch_poll(tbg_engine *engine, int *done);
+/* StateMachine.compact (:1148-1173) / checkpoint (:1175-1188). The forest's beat belongs to the
+ * replica; the engine's part is a barrier: every window committed so far is applied (and its
+ * write-back stream can be drained) once these return TBG_OK. */
+int tbg_compact(tbg_engine *engine, uint64_t op);
+int tbg_checkpoint(tbg_engine *engine);
+/* Whole-state digest for cross-replica determinism checks: out[0] accounts, out[1] transfers,
+ * out[2] pending statuses (position-sensitive 64-bit sums, tigerbeetle_amd/digest.py restates
+ * them), out[3] pulse_next_timestamp. Synchronizes. */
+int tbg_digest(tbg_engine *engine, uint64_t out[4]);
 
 /* Test hook mirroring the harness `setup` action (state_machine.zig:2545-2561). */
 int tbg_setup_balances(tbg_engine *engine, const tb_uint128_t *id, const tb_uint128_t *debits_pending,

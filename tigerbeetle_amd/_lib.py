@@ -18,6 +18,7 @@ EXPORTS = [
     "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4", "tbg_debug_counters", "tbg_shard_of",
     "tbg_shard_prepare_window", "tbg_shard_decide_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
     "tbg_shard_commit_bits_bytes", "tbg_window_changes", "tbg_windows_committed",
+    "tbg_open", "tbg_reset", "tbg_prefetch_poll", "tbg_compact", "tbg_checkpoint", "tbg_digest",
 ]
 
 
@@ -105,6 +106,12 @@ def lib():
         "tbg_window_changes": ([vp, vp, u64, P(u64), vp, u64, P(u64), vp, u64, P(u64)], i32),
         "tbg_shard_exchange_bytes": ([u32, u32], u64),
         "tbg_windows_committed": ([vp, P(u64), P(u64)], i32),
+        "tbg_open": ([vp, vp, u64, vp, u64, vp], i32),
+        "tbg_reset": ([vp], i32),
+        "tbg_prefetch_poll": ([vp, P(ctypes.c_int)], i32),
+        "tbg_compact": ([vp, u64], i32),
+        "tbg_checkpoint": ([vp], i32),
+        "tbg_digest": ([vp, P(u64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -87,7 +87,7 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t cand_count;
   uint32_t alt_count;
   uint32_t expired_count;
-  uint32_t pad2;
+  uint32_t pulse_done;  // k_pulse blocks finished (the last one runs the pulse's tail), reset by it
   uint64_t next_min;
   // walker statistics (cumulative)
   uint64_t w_events_total;
@@ -121,7 +121,27 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t x_id_max;    // >= every stored transfer id (u64 max once any id needs > 64 bits): an id
                         // above it cannot exist, so its table probe is skipped (monotonic ids)
   uint64_t windows_applied;  // create_* windows applied (rejected windows excluded), cumulative
+  uint32_t final_done;  // k_final blocks finished in a window with pulse_next ops (the last runs k_pn)
+  uint32_t pad4;
 };
+
+// Whether this block is the last of its grid to arrive (every thread of every block calls it once).
+// Every thread's earlier writes are released device-wide first, so the last block, after its
+// acquire, sees all of them; it resets the counter for the next launch. Costs an agent-scope fence
+// per block (an L2 writeback across the XCDs): only for rare paths.
+__device__ inline bool last_block_done(uint32_t* counter, uint32_t* flag_lds) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = atomicAdd(counter, 1u);
+    *flag_lds = prev == gridDim.x - 1 ? 1u : 0u;
+    if (*flag_lds) *counter = 0;
+  }
+  __syncthreads();
+  const bool last = *flag_lds != 0;
+  if (last) __threadfence();
+  return last;
+}
 
 // A rejected window (Globals::window_error bit 0) is skipped by every kernel that could change
 // state, and so is every window queued after it, until the host has seen the error (tbg_sync).

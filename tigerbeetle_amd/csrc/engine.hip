@@ -42,6 +42,7 @@
 #include "relax.h"
 #include "window.h"
 #include "changes.h"
+#include "restore.h"
 
 // k_final's streams, nontemporal: the window's event records (read for the last time) and the
 // inserted transfer records pass by, while the account table and records stay cached across windows
@@ -177,9 +178,12 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
             cls |= C_PV_PREBATCH;
             const tb_transfer_t p = d.xr[p_tslot];
             if ((p.flags & TB_TRANSFER_PENDING) && p.timeout > 0) {
-              // if it runs ok, it removes p's expires_at entry and may reset pulse_next (:1698-1708)
+              // if it runs ok, it removes p's expires_at entry and may reset pulse_next (:1698-1708):
+              // only if expires_at == pulse_next then, which is <= its value now (after this
+              // window's pulse; it only falls inside a window until a reset)
               pnv = expires_at_of(p);
               cls |= C_PNOP;
+              if (pnv <= d.g->pulse_next) atomicOr(&aux, 16u);
             }
             code = pv_against(t, p, &amt);
             if (p.flags & TB_TRANSFER_PENDING) {
@@ -325,7 +329,9 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
     if (aux & 1u) g->batch_huge = 1;
     const bool claim_free = !(aux & 2u);
     const bool prefix = claim_free && (aux & 4u) && g->x_sorted == g->x_count;
-    g->win_flags = (claim_free ? 1u : 0u) | (prefix ? 2u : 0u) | ((aux & 8u) ? 4u : 0u);
+    // bit 2: pulse_next ops; bit 3: a post/void that may reset pulse_next (k_final replays the
+    // window's ops in order only then; else pulse_next = min(itself, the creations that ran ok))
+    g->win_flags = (claim_free ? 1u : 0u) | (prefix ? 2u : 0u) | ((aux & 8u) ? 4u : 0u) | ((aux & 16u) ? 8u : 0u);
     // every balance field stays below 2^64 this window (k_walk computes the same for k_final; the
     // component walkers, which run before k_walk, read it from here)
     const u128 sum = g->ovf_bound + g->batch_amount_sum;
@@ -626,6 +632,178 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
 }
 
 // ------------------------------------------------------------------------------------------------
+// pulse_next_timestamp, exact (state_machine.zig:1576-1581, 1704-1708, 2112-2145). The reference
+// keeps it outside every groove, so a chain rollback undoes none of its edits:
+//   - every create_transfer that runs ok with a timeout lowers it to its expires_at (:1576-1581);
+//   - every post/void that runs ok on a pending transfer with a timeout resets it to timestamp_min
+//     when it equals that transfer's expires_at (:1704-1708).
+// Once reset, it stays timestamp_min until the next batch's pulse check (the harness pulses before
+// every batch, :2719-2739), where the pulse expires nothing (the window check guarantees it) and
+// its finish sets the first live expires_at or timestamp_max (:2126-2135). k_pn replays exactly
+// that over the window's ops in event order; events that ran ok are the committed ones plus the
+// rolled-back chain members marked C_RANOK.
+// ------------------------------------------------------------------------------------------------
+// The event's op: 0 none, 1 creation (value x), 2 reset candidate (value y).
+__device__ inline uint32_t pn_op(const Scratch& s, uint32_t i, uint64_t* v) {
+  const uint32_t cls = s.cls[i];
+  if (!(cls & C_PNOP)) return 0;
+  if (s.code[i] != TB_CT_OK && !(cls & C_RANOK)) return 0;
+  *v = s.pnv[i];
+  return (cls & C_POSTVOID) ? 2u : 1u;
+}
+
+__device__ inline unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
+
+// Block-wide minimum of a u64 (one LDS word per wave), result valid in every thread.
+template <int NWAVES>
+__device__ inline unsigned long long block_min_u64(unsigned long long v, unsigned long long* lds) {
+  return ~block_max_u64<NWAVES>(~v, lds);
+}
+
+// Exclusive prefix minimum over the block's threads (identity ~0); *total = the block minimum.
+template <int NWAVES>
+__device__ inline unsigned long long block_excl_min_u64(unsigned long long v, unsigned long long* lds,
+                                                        unsigned long long* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc = umin64(inc, y);
+  }
+  unsigned long long ex = __shfl_up(inc, 1, 64);
+  if (lane == 0) ex = ~0ull;
+  if (lane == 63) lds[wave] = inc;
+  __syncthreads();
+  unsigned long long wp = ~0ull, tot = ~0ull;
+#pragma unroll
+  for (int k = 0; k < NWAVES; k++) {
+    const unsigned long long x = lds[k];
+    if (k < wave) wp = umin64(wp, x);
+    tot = umin64(tot, x);
+  }
+  __syncthreads();
+  *total = tot;
+  return umin64(wp, ex);
+}
+
+// Per segment (one k_final block): the minimum creation value and the number of reset candidates
+// that can take effect before any in-window pulse, over the events that ran ok. Until the first
+// reset pulse_next only falls from pn0 (its value after the window's pulse), so a reset needs
+// expires_at <= pn0.
+__device__ inline void pn_seg_summary(const Scratch& s, uint32_t i, uint32_t E, uint64_t pn0, uint32_t* lds,
+                                      unsigned long long* ldsm) {
+  unsigned long long x = ~0ull;
+  uint32_t r = 0;
+  if (i < E) {
+    uint64_t v = 0;
+    const uint32_t op = pn_op(s, i, &v);
+    if (op == 1) x = v;
+    if (op == 2 && v <= pn0) r = 1;
+  }
+  const unsigned long long m = block_min_u64<SEG / 64>(x, ldsm);
+  const uint32_t n = block_sum<SEG / 64>(r, lds);
+  if (threadIdx.x == 0) {
+    s.pn_min[blockIdx.x] = m;
+    s.pn_res[blockIdx.x] = n;
+  }
+}
+
+#define PN_THREADS 1024
+
+// The pulse at the start of batch b >= 1 after a reset: nothing is due (window check), so its
+// finish sets the minimum expires_at among the entries live at that point, else timestamp_max.
+// Live then = (A) entries pending now and created before batch b (pre-window slots, or records
+// stamped <= T_{b-1}), plus (B) pending transfers that a committed post/void of batch >= b removed,
+// created before batch b. Rare (a reset inside a multi-batch window): one workgroup, plain loops.
+__device__ uint64_t pn_minlive(const Dev& d, const Scratch& s, const WinDesc& w, uint32_t b,
+                               unsigned long long* ldsm) {
+  const uint64_t base = d.g->base;
+  const uint64_t t_prev = w.T[b - 1];
+  unsigned long long m = ~0ull;
+  const ExpEntry* list = d.exp[*d.exp_cur];
+  const uint64_t cnt = d.g->exp_count;
+  for (uint64_t j = threadIdx.x; j < cnt; j += PN_THREADS) {
+    const ExpEntry e = list[j];
+    if (d.xstatus[e.slot] != TB_PENDING_PENDING) continue;
+    if (e.slot >= base && d.xr[e.slot].timestamp > t_prev) continue;  // created in batch >= b
+    m = umin64(m, e.expires_at);
+  }
+  for (uint32_t k = w.off[b] + threadIdx.x; k < w.E; k += PN_THREADS) {
+    const uint32_t cls = s.cls[k];
+    if (!(cls & C_POSTVOID) || !(cls & C_PNOP) || s.code[k] != TB_CT_OK) continue;
+    uint64_t pts;
+    const uint32_t ps = s.p_tslot[k];
+    if (ps != NONE32) {
+      pts = d.xr[ps].timestamp;  // created before the window
+    } else {
+      const uint32_t pc = s.pn_src[k];
+      if (s.batch[pc] >= b) continue;
+      pts = win_ts(w, s.batch[pc], pc);
+    }
+    const uint64_t y = s.pnv[k];
+    if ((pts >> 63) || y > TB_TIMESTAMP_MAX) continue;  // never visible to the scan (composite key)
+    m = umin64(m, y);
+  }
+  m = block_min_u64<PN_THREADS / 64>(m, ldsm);
+  return m == ~0ull ? TB_TIMESTAMP_MAX : m;
+}
+
+// The replay, by the last k_final block of a window with pulse_next ops (PN_THREADS threads).
+__device__ void pn_replay(const Dev& d, const Scratch& s, const WinDesc& w, unsigned long long* ldsm,
+                          uint32_t* sh) {
+  uint32_t& first_eff = sh[0];
+  uint32_t& next_seg = sh[1];
+  const uint32_t E = w.E, nseg = (E + SEG - 1) / SEG;
+  const uint64_t pn0 = d.g->pulse_next;  // after the pulse before the window
+  uint64_t pn = pn0;
+  // after an in-window pulse pulse_next may exceed pn0: the segment summaries (resets <= pn0) no
+  // longer bound the candidates, so every later event is replayed one by one
+  bool all_events = false;
+  uint32_t i = 0;
+  while (i < E) {
+    if (i % SEG == 0 && !all_events) {
+      // fold whole segments without a reset candidate; stop at the next one that has some
+      const uint32_t s0 = i / SEG;
+      if (threadIdx.x == 0) next_seg = NONE32;
+      __syncthreads();
+      for (uint32_t j = s0 + threadIdx.x; j < nseg; j += PN_THREADS)
+        if (s.pn_res[j]) atomicMin(&next_seg, j);
+      __syncthreads();
+      const uint32_t stop = next_seg == NONE32 ? nseg : next_seg;
+      unsigned long long m = ~0ull;
+      for (uint32_t j = s0 + threadIdx.x; j < stop; j += PN_THREADS) m = umin64(m, s.pn_min[j]);
+      pn = umin64(pn, block_min_u64<PN_THREADS / 64>(m, ldsm));
+      if (stop == nseg) break;
+      i = stop * SEG;
+    }
+    // event by event, within one segment and one batch
+    const uint32_t b = s.batch[i];
+    const uint32_t end = min(min((i / SEG + 1) * SEG, E), w.off[b + 1]);
+    const uint32_t k = i + threadIdx.x;
+    uint64_t v = 0;
+    const uint32_t op = k < end ? pn_op(s, k, &v) : 0u;
+    unsigned long long tot;
+    const unsigned long long before = umin64(pn, block_excl_min_u64<PN_THREADS / 64>(op == 1 ? v : ~0ull, ldsm, &tot));
+    if (threadIdx.x == 0) first_eff = NONE32;
+    __syncthreads();
+    if (op == 2 && before == v) atomicMin(&first_eff, k);
+    __syncthreads();
+    if (first_eff != NONE32) {
+      // reset to timestamp_min (:1706-1707); the next batch's pulse finds nothing due
+      i = w.off[b + 1];
+      pn = b + 1 < w.nb ? pn_minlive(d, s, w, b + 1, ldsm) : TB_TIMESTAMP_MIN;
+      all_events = all_events || pn > pn0;
+    } else {
+      pn = umin64(pn, tot);
+      i = end;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) d.g->pulse_next = pn;
+}
+
+// ------------------------------------------------------------------------------------------------
 // final: ordered replies + insert ranks + effects (one event per thread, one segment per block)
 // ------------------------------------------------------------------------------------------------
 struct FinalOut {
@@ -898,173 +1076,19 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     gw->light_count = 0;
     gw->cpw_done = 0;
   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// pulse_next_timestamp, exact (state_machine.zig:1576-1581, 1704-1708, 2112-2145). The reference
-// keeps it outside every groove, so a chain rollback undoes none of its edits:
-//   - every create_transfer that runs ok with a timeout lowers it to its expires_at (:1576-1581);
-//   - every post/void that runs ok on a pending transfer with a timeout resets it to timestamp_min
-//     when it equals that transfer's expires_at (:1704-1708).
-// Once reset, it stays timestamp_min until the next batch's pulse check (the harness pulses before
-// every batch, :2719-2739), where the pulse expires nothing (the window check guarantees it) and
-// its finish sets the first live expires_at or timestamp_max (:2126-2135). k_pn replays exactly
-// that over the window's ops in event order; events that ran ok are the committed ones plus the
-// rolled-back chain members marked C_RANOK.
-// ------------------------------------------------------------------------------------------------
-// The event's op: 0 none, 1 creation (value x), 2 reset candidate (value y).
-__device__ inline uint32_t pn_op(const Scratch& s, uint32_t i, uint64_t* v) {
-  const uint32_t cls = s.cls[i];
-  if (!(cls & C_PNOP)) return 0;
-  if (s.code[i] != TB_CT_OK && !(cls & C_RANOK)) return 0;
-  *v = s.pnv[i];
-  return (cls & C_POSTVOID) ? 2u : 1u;
-}
-
-__device__ inline unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
-
-// Block-wide minimum of a u64 (one LDS word per wave), result valid in every thread.
-template <int NWAVES>
-__device__ inline unsigned long long block_min_u64(unsigned long long v, unsigned long long* lds) {
-  return ~block_max_u64<NWAVES>(~v, lds);
-}
-
-// Exclusive prefix minimum over the block's threads (identity ~0); *total = the block minimum.
-template <int NWAVES>
-__device__ inline unsigned long long block_excl_min_u64(unsigned long long v, unsigned long long* lds,
-                                                        unsigned long long* total) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned long long inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc = umin64(inc, y);
-  }
-  unsigned long long ex = __shfl_up(inc, 1, 64);
-  if (lane == 0) ex = ~0ull;
-  if (lane == 63) lds[wave] = inc;
-  __syncthreads();
-  unsigned long long wp = ~0ull, tot = ~0ull;
-#pragma unroll
-  for (int k = 0; k < NWAVES; k++) {
-    const unsigned long long x = lds[k];
-    if (k < wave) wp = umin64(wp, x);
-    tot = umin64(tot, x);
-  }
-  __syncthreads();
-  *total = tot;
-  return umin64(wp, ex);
-}
-
-// Per segment: the minimum creation value and the number of reset candidates, over the events
-// that ran ok. Only windows whose prep saw a candidate (win_flags bit 2) do any work.
-__global__ void __launch_bounds__(SEG) k_pn_seg(Dev d, Scratch s, uint32_t E) {
-  __shared__ uint32_t lds[SEG / 64];
-  __shared__ unsigned long long ldsm[SEG / 64];
-  if (WIN_REJECTED(d.g) || !(d.g->win_flags & 4u)) return;
-  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
-  unsigned long long x = ~0ull;
-  uint32_t r = 0;
-  if (i < E) {
+  const uint32_t wf = XFER ? d.g->win_flags : 0u;
+  if (wf & 8u) {
+    // a post/void may reset pulse_next: this segment's summary, then the last block to finish
+    // replays the window's ops in event order into pulse_next
+    __shared__ uint32_t pn_sh[3];
+    pn_seg_summary(s, i, E, d.g->pulse_next, lds, ldsm);
+    if (last_block_done(&d.g->final_done, &pn_sh[2])) pn_replay(d, s, w, ldsm, pn_sh);
+  } else if (wf & 4u) {
+    // no reset possible: pulse_next = min(pulse_next, every creation that ran ok) (:1576-1581)
     uint64_t v = 0;
-    const uint32_t op = pn_op(s, i, &v);
-    if (op == 1) x = v;
-    if (op == 2) r = 1;
+    const unsigned long long m = block_min_u64<SEG / 64>((i < E && pn_op(s, i, &v) == 1) ? v : ~0ull, ldsm);
+    if (threadIdx.x == 0 && m != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(&d.g->pulse_next), m);
   }
-  const unsigned long long m = block_min_u64<SEG / 64>(x, ldsm);
-  const uint32_t n = block_sum<SEG / 64>(r, lds);
-  if (threadIdx.x == 0) {
-    s.pn_min[blockIdx.x] = m;
-    s.pn_res[blockIdx.x] = n;
-  }
-}
-
-#define PN_THREADS 1024
-
-// The pulse at the start of batch b >= 1 after a reset: nothing is due (window check), so its
-// finish sets the minimum expires_at among the entries live at that point, else timestamp_max.
-// Live then = (A) entries pending now and created before batch b (pre-window slots, or records
-// stamped <= T_{b-1}), plus (B) pending transfers that a committed post/void of batch >= b removed,
-// created before batch b. Rare (a reset inside a multi-batch window): one workgroup, plain loops.
-__device__ uint64_t pn_minlive(const Dev& d, const Scratch& s, const WinDesc& w, uint32_t b,
-                               unsigned long long* ldsm) {
-  const uint64_t base = d.g->base;
-  const uint64_t t_prev = w.T[b - 1];
-  unsigned long long m = ~0ull;
-  const ExpEntry* list = d.exp[*d.exp_cur];
-  const uint64_t cnt = d.g->exp_count;
-  for (uint64_t j = threadIdx.x; j < cnt; j += PN_THREADS) {
-    const ExpEntry e = list[j];
-    if (d.xstatus[e.slot] != TB_PENDING_PENDING) continue;
-    if (e.slot >= base && d.xr[e.slot].timestamp > t_prev) continue;  // created in batch >= b
-    m = umin64(m, e.expires_at);
-  }
-  for (uint32_t k = w.off[b] + threadIdx.x; k < w.E; k += PN_THREADS) {
-    const uint32_t cls = s.cls[k];
-    if (!(cls & C_POSTVOID) || !(cls & C_PNOP) || s.code[k] != TB_CT_OK) continue;
-    uint64_t pts;
-    const uint32_t ps = s.p_tslot[k];
-    if (ps != NONE32) {
-      pts = d.xr[ps].timestamp;  // created before the window
-    } else {
-      const uint32_t pc = s.pn_src[k];
-      if (s.batch[pc] >= b) continue;
-      pts = win_ts(w, s.batch[pc], pc);
-    }
-    const uint64_t y = s.pnv[k];
-    if ((pts >> 63) || y > TB_TIMESTAMP_MAX) continue;  // never visible to the scan (composite key)
-    m = umin64(m, y);
-  }
-  m = block_min_u64<PN_THREADS / 64>(m, ldsm);
-  return m == ~0ull ? TB_TIMESTAMP_MAX : m;
-}
-
-__global__ void __launch_bounds__(PN_THREADS) k_pn(Dev d, Scratch s, WinDesc w) {
-  __shared__ unsigned long long ldsm[PN_THREADS / 64];
-  __shared__ uint32_t first_eff, next_seg;
-  if (WIN_REJECTED(d.g) || !(d.g->win_flags & 4u)) return;
-  const uint32_t E = w.E, nseg = (E + SEG - 1) / SEG;
-  uint64_t pn = d.g->pulse_next;  // after the pulse before the window
-  uint32_t i = 0;
-  while (i < E) {
-    if (i % SEG == 0) {
-      // fold whole segments without a reset candidate; stop at the next one that has some
-      const uint32_t s0 = i / SEG;
-      if (threadIdx.x == 0) next_seg = NONE32;
-      __syncthreads();
-      for (uint32_t j = s0 + threadIdx.x; j < nseg; j += PN_THREADS)
-        if (s.pn_res[j]) atomicMin(&next_seg, j);
-      __syncthreads();
-      const uint32_t stop = next_seg == NONE32 ? nseg : next_seg;
-      unsigned long long m = ~0ull;
-      for (uint32_t j = s0 + threadIdx.x; j < stop; j += PN_THREADS) m = umin64(m, s.pn_min[j]);
-      pn = umin64(pn, block_min_u64<PN_THREADS / 64>(m, ldsm));
-      if (stop == nseg) break;
-      i = stop * SEG;
-    }
-    // event by event, within one segment and one batch
-    const uint32_t b = s.batch[i];
-    const uint32_t end = min(min((i / SEG + 1) * SEG, E), w.off[b + 1]);
-    const uint32_t k = i + threadIdx.x;
-    uint64_t v = 0;
-    const uint32_t op = k < end ? pn_op(s, k, &v) : 0u;
-    unsigned long long tot;
-    const unsigned long long before = umin64(pn, block_excl_min_u64<PN_THREADS / 64>(op == 1 ? v : ~0ull, ldsm, &tot));
-    if (threadIdx.x == 0) first_eff = NONE32;
-    __syncthreads();
-    if (op == 2 && before == v) atomicMin(&first_eff, k);
-    __syncthreads();
-    if (first_eff != NONE32) {
-      // reset to timestamp_min (:1706-1707); the next batch's pulse finds nothing due
-      i = w.off[b + 1];
-      pn = b + 1 < w.nb ? pn_minlive(d, s, w, b + 1, ldsm) : TB_TIMESTAMP_MIN;
-    } else {
-      pn = umin64(pn, tot);
-      i = end;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) d.g->pulse_next = pn;
 }
 
 #include "shard.h"
@@ -1074,11 +1098,6 @@ __global__ void __launch_bounds__(PN_THREADS) k_pn(Dev d, Scratch s, WinDesc w) 
 // 1010-1105, 1874-1929, 2112-2166). The live list holds scan-visible pending-with-timeout entries;
 // an entry is live while its transfer's status is `pending`.
 // ------------------------------------------------------------------------------------------------
-struct PulseCtl {
-  uint32_t active;
-  uint32_t pad;
-};
-
 // The window a pulse decision precedes: a window of several batches is valid only if no pulse can
 // fall due inside it (the harness runs a pulse check before every batch, state_machine.zig:
 // 2719-2739). Live expires_at entries are >= pulse_next (an invariant of the reference value too:
@@ -1092,58 +1111,51 @@ __device__ inline bool window_spans_pulse(const WinChk& c, uint64_t pulse_next) 
   return c.nb > 1 && (c.T_last >= pulse_next || c.T_last >= c.first_ts + TB_NS_PER_S);
 }
 
-// pulse() (:589-596) and the expires_at scan (:1010-1043, value_next :2147-2166): the due live
-// entries go to `cand`, the others to the alternate list. When no pulse runs, block 0 checks the
-// window against the current pulse_next; a window that spans a due pulse is rejected whole
-// (window_error bit 0): it and every window after it change nothing until tbg_sync reports it.
-// Counters (cand_count, alt_count, next_min) are zero here: k_pulse_tail leaves them so.
-__global__ void __launch_bounds__(256) k_pulse_scan(Dev d, Scratch s, PulseCtl* ctl, uint64_t T,
-                                                    uint64_t prepare_timestamp, WinChk chk) {
-  const bool first = blockIdx.x == 0 && threadIdx.x == 0;
-  if (WIN_REJECTED(d.g)) {
-    if (first) ctl->active = 0;
-    return;
-  }
-  const uint64_t pn = d.g->pulse_next;
-  const bool active = pn <= prepare_timestamp;
-  if (first) {
-    ctl->active = active ? 1u : 0u;
-    if (!active && window_spans_pulse(chk, pn)) atomicOr(&d.g->window_error, 1u);
-  }
-  if (!active) return;
-  const uint32_t cur = *d.exp_cur;
-  const ExpEntry* list = d.exp[cur];
-  ExpEntry* alt = d.exp[cur ^ 1];
-  const uint64_t count = d.g->exp_count;
-  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < count; j += (uint64_t)gridDim.x * blockDim.x) {
-    const ExpEntry e = list[j];
-    if (d.xstatus[e.slot] != TB_PENDING_PENDING) continue;  // removed from the index
-    if (e.expires_at <= T) {
-      const uint32_t k = atomicAdd(&d.g->cand_count, 1u);
-      s.cand[k] = e;
-    } else {
-      const uint32_t k = atomicAdd(&d.g->alt_count, 1u);
-      alt[k] = e;
-      atomicMin(reinterpret_cast<unsigned long long*>(&d.g->next_min), (unsigned long long)e.expires_at);
-    }
-  }
-}
-
-// One workgroup: selection of the `cap` smallest (expires_at, slot) keys when more are due (12-pass
-// LDS radix select, 8-bit digits over the 96-bit key; slot order = timestamp order), the finish
-// (:2112-2145) into pulse_next, the window check against that new value, then
-// execute_expire_pending_transfers (:1874-1929) and the list swap. A rejected window leaves
-// everything as it was: the scan only read the live list.
-__global__ void __launch_bounds__(1024) k_pulse_tail(Dev d, Scratch s, PulseCtl* ctl, uint32_t cap, ChgLog chg,
-                                                    uint32_t chg_epoch, WinChk chk) {
+// The pulse before a window, in one launch: pulse() (:589-596), the expires_at scan (:1010-1043,
+// value_next :2147-2166) over the live list by the whole grid (due entries to `cand`, the others to
+// the alternate list), then, in the last block to finish: selection of the `cap` smallest
+// (expires_at, slot) keys when more are due (12-pass LDS radix select, 8-bit digits over the 96-bit
+// key; slot order = timestamp order), the finish (:2112-2145) into pulse_next, the window check
+// against that new value, execute_expire_pending_transfers (:1874-1929) and the list swap.
+// When no pulse is due every block returns at once, block 0 having checked the window against the
+// current pulse_next. A window that spans a due pulse is rejected whole (window_error bit 0): it and
+// every window after it change nothing until tbg_sync reports it; the scan only read the live list,
+// so a rejected pulse leaves everything as it was. cand_count, alt_count and next_min are zero on
+// entry (the tail leaves them so).
+#define PULSE_BLOCKS 16  // few blocks: each pays an agent-scope fence before the last one runs the tail
+__global__ void __launch_bounds__(1024) k_pulse(Dev d, Scratch s, uint64_t T, uint64_t prepare_timestamp,
+                                               uint32_t cap, ChgLog chg, uint32_t chg_epoch, WinChk chk) {
   __shared__ uint32_t hist[256];
   __shared__ uint64_t prefix_hi;
   __shared__ uint32_t prefix_lo;
   __shared__ uint32_t want;
-  __shared__ uint32_t reject;
-  if (!ctl->active) return;
+  __shared__ uint32_t flag;
   Globals* g = d.g;
-  const uint32_t m = g->cand_count;
+  if (WIN_REJECTED(g)) return;
+  const uint64_t pn = g->pulse_next;
+  if (!(pn <= prepare_timestamp)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && window_spans_pulse(chk, pn)) atomicOr(&g->window_error, 1u);
+    return;
+  }
+  const uint32_t cur = *d.exp_cur;
+  const ExpEntry* list = d.exp[cur];
+  ExpEntry* alt = d.exp[cur ^ 1];
+  const uint64_t count = g->exp_count;
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < count; j += (uint64_t)gridDim.x * blockDim.x) {
+    const ExpEntry e = list[j];
+    if (d.xstatus[e.slot] != TB_PENDING_PENDING) continue;  // removed from the index
+    if (e.expires_at <= T) {
+      const uint32_t k = atomicAdd(&g->cand_count, 1u);
+      s.cand[k] = e;
+    } else {
+      const uint32_t k = atomicAdd(&g->alt_count, 1u);
+      alt[k] = e;
+      atomicMin(reinterpret_cast<unsigned long long*>(&g->next_min), (unsigned long long)e.expires_at);
+    }
+  }
+  if (!last_block_done(&g->pulse_done, &flag)) return;
+  // ---- the last block: selection, finish, window check, apply ----
+  const uint32_t m = __hip_atomic_load(&g->cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool select_all = m <= cap;
   if (threadIdx.x == 0) {
     prefix_hi = 0;
@@ -1188,24 +1200,20 @@ __global__ void __launch_bounds__(1024) k_pulse_tail(Dev d, Scratch s, PulseCtl*
   }
   // finish: scan_finished -> the first live entry beyond T, else timestamp_max; buffer_finished ->
   // the last included expires_at (another pulse follows)
-  const uint64_t pn_after =
-      select_all ? (g->alt_count > 0 ? g->next_min : TB_TIMESTAMP_MAX) : prefix_hi;
+  const uint32_t n_alt = __hip_atomic_load(&g->alt_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t pn_after = select_all ? (n_alt > 0 ? g->next_min : TB_TIMESTAMP_MAX) : prefix_hi;
   const uint64_t thr_e = prefix_hi;
   const uint32_t thr_s = prefix_lo;
-  if (threadIdx.x == 0) reject = window_spans_pulse(chk, pn_after) ? 1u : 0u;
-  __syncthreads();
-  if (reject) {
+  if (window_spans_pulse(chk, pn_after)) {
+    __syncthreads();
     if (threadIdx.x == 0) {
       atomicOr(&g->window_error, 1u);
       g->cand_count = 0;
       g->alt_count = 0;
       g->next_min = ~0ull;
-      ctl->active = 0;
     }
     return;
   }
-  const uint32_t cur = *d.exp_cur;
-  ExpEntry* alt = d.exp[cur ^ 1];
   for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
     const ExpEntry e = s.cand[j];
     const bool take = select_all || e.expires_at < thr_e || (e.expires_at == thr_e && e.slot <= thr_s);
@@ -1237,7 +1245,6 @@ __global__ void __launch_bounds__(1024) k_pulse_tail(Dev d, Scratch s, PulseCtl*
     g->cand_count = 0;
     g->alt_count = 0;
     g->next_min = ~0ull;
-    ctl->active = 0;
   }
 }
 

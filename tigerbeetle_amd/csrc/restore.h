@@ -1,0 +1,101 @@
+// restore.h — engine state from the LSM forest's objects (StateMachine.open after a restart or a
+// state sync, state_machine.zig:527-541, 486-501) and the whole-state digest.
+//
+// open: the grooves hold every Account and Transfer object and every TransferPending row; the
+// engine is rebuilt from them in timestamp order (= its dense store order): the records are copied
+// into the stores, the id tables are rebuilt, the TransferPending status lands per transfer slot,
+// and the live expires_at list is every pending transfer with a scan-visible timeout
+// (state_machine.zig:229-238, lsm/composite_key.zig:47-49). pulse_next_timestamp starts at
+// timestamp_min as in a freshly initialised StateMachine (:2063): the first pulse scans.
+#pragma once
+#include "window.h"
+
+// Upper bound of every balance sum (dp + dpo, cp + cpo) of the loaded accounts: max of the high
+// words (with a saturation flag) and max of the low words among sums below 2^64 (ovf_bound only has
+// to be >= every sum; a looser bound only sends more windows down the exact overflow path).
+struct LoadBound {
+  unsigned long long hi_max;  // max high word of any sum; ~0 = a sum wrapped 128 bits
+  unsigned long long lo_max;  // max of the sums that fit 64 bits
+};
+
+__global__ void __launch_bounds__(256) k_load_accounts(Dev d, uint64_t first, uint64_t n, LoadBound* lb) {
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t slot = first + k;
+    const tb_account_t a = d.acc[slot];
+    acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
+    d.hot[slot] = 0;
+    if (a.flags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS | TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS))
+      atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->limited_accounts), 1ull);
+    const u128 dp = U(a.debits_pending), cp = U(a.credits_pending);
+    const u128 s1 = dp + U(a.debits_posted), s2 = cp + U(a.credits_posted);
+    const bool sat = s1 < dp || s2 < cp;
+    const u128 m = s1 > s2 ? s1 : s2;
+    const unsigned long long hi = sat ? ~0ull : (unsigned long long)(m >> 64);
+    if (hi) atomicMax(&lb->hi_max, hi);
+    else atomicMax(&lb->lo_max, (unsigned long long)m);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_load_transfers(Dev d, uint64_t first, uint64_t n) {
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t slot = first + k;
+    const tb_transfer_t t = d.xr[slot];
+    x_insert(d.x_tab, d.x_mask, t.id, (uint32_t)slot);
+    atomicMax(reinterpret_cast<unsigned long long*>(&d.g->x_id_max), (unsigned long long)x_id_key(t.id));
+    if (!(t.flags & TB_TRANSFER_PENDING) || t.timeout == 0 || d.xstatus[slot] != TB_PENDING_PENDING) continue;
+    const uint64_t expires_at = expires_at_of(t);
+    if ((t.timestamp >> 63) || expires_at > TB_TIMESTAMP_MAX) continue;  // never visible to the scan
+    ExpEntry e;
+    e.expires_at = expires_at;
+    e.slot = (uint32_t)slot;
+    e.pad = 0;
+    const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), 1ull);
+    d.exp[*d.exp_cur][q] = e;
+  }
+}
+
+__global__ void k_load_finish(Dev d, const LoadBound* lb, uint64_t n_acc, uint64_t n_x) {
+  Globals* g = d.g;
+  g->acc_count = n_acc;
+  g->x_count = n_x;
+  g->x_sorted = 0;  // every loaded transfer is hashed
+  g->mono_prev = 0;
+  g->pulse_next = TB_TIMESTAMP_MIN;
+  if (lb->hi_max == ~0ull)
+    g->ovf_bound = MAX128;
+  else if (lb->hi_max)
+    g->ovf_bound = ((u128)lb->hi_max << 64) | (u128)~0ull;
+  else
+    g->ovf_bound = lb->lo_max;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Digest: a position-sensitive 64-bit sum over the dense stores (every 8-byte word of every record,
+// each record mixed with its slot), the pending statuses and pulse_next_timestamp. Replicas holding
+// the same state have the same digest; tests recompute it from the CPU restatement's dumps
+// (tigerbeetle_amd/digest.py).
+// ------------------------------------------------------------------------------------------------
+__device__ inline unsigned long long digest_record(const uint64_t* w, uint64_t slot) {
+  unsigned long long h = 0x243f6a8885a308d3ull ^ slot;
+#pragma unroll
+  for (int k = 0; k < 16; k++) h = mix64(h ^ w[k] ^ ((unsigned long long)k << 56));
+  return mix64(h + slot * 0x9e3779b97f4a7c15ull);
+}
+
+__global__ void __launch_bounds__(256) k_digest(const uint8_t* records, uint64_t n, const uint8_t* status,
+                                                unsigned long long* out) {
+  unsigned long long sr = 0, ss = 0;
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    sr += digest_record(reinterpret_cast<const uint64_t*>(records + k * 128), k);
+    if (status) ss += mix64((k << 8) | status[k]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sr += __shfl_xor(sr, o, 64);
+    ss += __shfl_xor(ss, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&out[0], sr);
+    if (status) atomicAdd(&out[1], ss);
+  }
+}

@@ -160,6 +160,39 @@ class StateMachine:
     def sync(self):
         _lib.check(_lib.lib().tbg_sync(self.h), "sync")
 
+    # ---- the rest of the reference surface the replica drives ------------------------------
+    def open(self, accounts, transfers, pending_status):
+        """StateMachine.open (state_machine.zig:527-541): an empty engine takes the forest's objects
+        (records in timestamp order, one TransferPending status per transfer)."""
+        acc = np.ascontiguousarray(accounts)
+        xf = np.ascontiguousarray(transfers)
+        st = np.ascontiguousarray(pending_status, dtype=np.uint8)
+        _lib.check(_lib.lib().tbg_open(self.h, acc.ctypes.data if len(acc) else None, len(acc),
+                                       xf.ctypes.data if len(xf) else None, len(xf),
+                                       st.ctypes.data if len(st) else None), "open")
+
+    def reset(self):
+        """StateMachine.reset (state_machine.zig:486-501)."""
+        _lib.check(_lib.lib().tbg_reset(self.h), "reset")
+        self.prepare_timestamp = self.prefetch_timestamp = self.commit_timestamp = 0
+
+    def prefetch_done(self):
+        done = ctypes.c_int()
+        _lib.check(_lib.lib().tbg_prefetch_poll(self.h, ctypes.byref(done)), "prefetch_poll")
+        return bool(done.value)
+
+    def compact(self, op):
+        _lib.check(_lib.lib().tbg_compact(self.h, op), "compact")
+
+    def checkpoint(self):
+        _lib.check(_lib.lib().tbg_checkpoint(self.h), "checkpoint")
+
+    def digest(self):
+        """tbg_digest: [accounts, transfers, statuses, pulse_next_timestamp] (tigerbeetle_amd.digest)."""
+        out = (ctypes.c_uint64 * 4)()
+        _lib.check(_lib.lib().tbg_digest(self.h, out), "digest")
+        return list(out)
+
     def windows_committed(self):
         """(applied, submitted) create_* windows since creation (tbg_windows_committed)."""
         a, s = ctypes.c_uint64(), ctypes.c_uint64()
