@@ -830,3 +830,12 @@ uint32_t tbo_pending_status(tbo_state *s, uint64_t timestamp) {
     int slot = get_pending_slot(s, timestamp);
     return slot < 0 ? 0 : s->pend_status[slot];
 }
+/* Pending status of every stored transfer, in store (= timestamp) order; 0 = none. */
+uint64_t tbo_dump_transfer_status(tbo_state *s, uint8_t *out, uint64_t cap) {
+    uint64_t n = s->xfer_n < cap ? s->xfer_n : cap;
+    for (uint64_t i = 0; i < n; i++) {
+        int slot = get_pending_slot(s, s->xfer[i].timestamp);
+        out[i] = slot < 0 ? 0 : s->pend_status[slot];
+    }
+    return n;
+}

@@ -58,6 +58,8 @@ def lib():
         L.tbo_pending_status.argtypes = [vp, u64]
         L.tbo_pending_status.restype = u32
         L.tbo_input_valid.argtypes = [u32, u64, u32]
+        L.tbo_dump_transfer_status.argtypes = [vp, vp, u64]
+        L.tbo_dump_transfer_status.restype = u64
         _lib = L
     return _lib
 
@@ -134,4 +136,11 @@ class OracleStateMachine:
         n = L.tbo_transfer_count(self.h)
         out = np.zeros(max(n, 1), TRANSFER_DTYPE)
         L.tbo_dump_transfers(self.h, out.ctypes.data, n)
+        return out[:n]
+
+    def dump_transfer_status(self):
+        L = lib()
+        n = L.tbo_transfer_count(self.h)
+        out = np.zeros(max(n, 1), np.uint8)
+        L.tbo_dump_transfer_status(self.h, out.ctypes.data, n)
         return out[:n]

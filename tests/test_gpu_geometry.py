@@ -1,0 +1,177 @@
+"""Parity at the bench's own geometry (bench.py): 1M accounts and 128-batch windows of 8190-event
+batches (~1M events per window), the windows bench.py commits; the GPU engine vs the CPU
+restatement batch by batch under the harness protocol. Replies per batch, then the stores: byte for
+byte and through the whole-state digest (tbg_digest vs tigerbeetle_amd.digest over the oracle's
+dumps).
+
+- cfg2: uniform transfers, device-generated exactly as bench.py generates them;
+- cfg4 mixed at window scale: two-phase, posts/voids, chains with injected failures in 1M-event
+  windows (no tick inside a window: the component walkers and the pulse_next replay at scale);
+- cfg3: Zipf(1.2) with limits, pre-funded, bench.py's 32-batch windows (the account-parallel
+  resolver at 262K-event windows);
+- cfg5: G = 8 hash shards on one GPU at 128-batch windows, 12.5M accounts' shape scaled to 1M.
+"""
+import numpy as np
+import pytest
+
+from oracle_sm import OracleStateMachine
+from test_gpu_parity import _compare_final
+from test_gpu_window import commit_window, oracle_batches
+from tigerbeetle_amd import workload
+from tigerbeetle_amd.digest import digest
+from tigerbeetle_amd.state_machine import to_host
+from tigerbeetle_amd.types import Operation
+
+BM = 8190
+N_ACC = 1_000_000
+
+
+def _batches(arr, first=0, count=None):
+    count = len(arr) if count is None else count
+    return [arr[i:i + BM] for i in range(first, first + count, BM)]
+
+
+def _check_digest(gpu, ref):
+    rx = ref.dump_transfers()
+    want = digest(ref.dump_accounts(), rx, ref.dump_transfer_status(), ref.pulse_next_timestamp())
+    assert gpu.digest() == want
+
+
+def _accounts(gpu, ref, seed):
+    acc = _batches(workload.accounts(0, N_ACC, seed))
+    for w0 in range(0, len(acc), 128):
+        assert commit_window(gpu, Operation.create_accounts, acc[w0:w0 + 128]) == \
+            oracle_batches(ref, Operation.create_accounts, acc[w0:w0 + 128])
+
+
+@pytest.mark.gpu
+def test_geometry_cfg2_uniform():
+    """bench.py's cfg2 path: device-generated stream, tbg_commit_window over 128 batches."""
+    import torch
+
+    from tigerbeetle_amd import StateMachine, _lib
+
+    L = _lib.lib()
+    n_win, seed = 3, 44
+    n_x = n_win * 128 * BM
+    gpu = StateMachine(batch_max=BM, accounts_max=N_ACC, transfers_max=n_x, window_events_max=128 * BM)
+    ref = OracleStateMachine(batch_max=BM)
+    try:
+        _accounts(gpu, ref, seed)
+        d_x = torch.empty(n_x * 128, dtype=torch.uint8, device="cuda")
+        d_res = torch.zeros(128 * BM * 8, dtype=torch.uint8, device="cuda")
+        d_base = torch.zeros(129, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        _lib.check(L.tbg_gen_transfers_uniform(d_x.data_ptr(), 0, n_x, seed, N_ACC, 0, gpu.stream), "gen")
+        host = workload.transfers_uniform(0, n_x, seed, N_ACC)
+        for w in range(n_win):
+            ns, ts = [], []
+            for _ in range(128):
+                gpu.prepare_timestamp += 1 + BM
+                ns.append(BM)
+                ts.append(gpu.prepare_timestamp)
+            gpu.commit_window(Operation.create_transfers, d_x.data_ptr() + w * 128 * BM * 128, ns, ts,
+                              d_res.data_ptr(), d_base.data_ptr(), True, ts[0])
+            gpu.sync()
+            base = to_host(d_base)
+            res = to_host(d_res).tobytes()
+            r = oracle_batches(ref, Operation.create_transfers, _batches(host, w * 128 * BM, 128 * BM))
+            assert [res[base[b] * 8: base[b + 1] * 8] for b in range(128)] == r
+        assert gpu.stats()["transfers"] == n_x
+        _check_digest(gpu, ref)
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_geometry_cfg4_mixed_windows():
+    """cfg4's event mix (30 % pending with timeouts, posts/voids of earlier pending transfers, 10 %
+    of events in chains with injected failures) in 128-batch windows on 1M accounts."""
+    from tigerbeetle_amd import StateMachine
+
+    n_win, seed = 2, 46
+    n_x = n_win * 128 * BM
+    gpu = StateMachine(batch_max=BM, accounts_max=N_ACC, transfers_max=n_x, window_events_max=128 * BM)
+    ref = OracleStateMachine(batch_max=BM)
+    try:
+        _accounts(gpu, ref, seed)
+        host = workload.transfers_cfg4(0, n_x, seed, N_ACC, BM)
+        for w in range(n_win):
+            xb = _batches(host, w * 128 * BM, 128 * BM)
+            g = commit_window(gpu, Operation.create_transfers, xb)
+            r = oracle_batches(ref, Operation.create_transfers, xb)
+            bad = [b for b in range(128) if g[b] != r[b]]
+            assert not bad, f"window {w}: batches {bad[:8]} differ"
+            assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
+        st = gpu.stats()
+        assert st["component_events"] + st["walker_events"] > 0  # the order-dependent part ran
+        _check_digest(gpu, ref)
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_geometry_cfg3_zipf_limits():
+    """bench.py's cfg3: Zipf(1.2) with debits_must_not_exceed_credits limits, funded from treasury
+    accounts, 32-batch windows."""
+    from tigerbeetle_amd import StateMachine
+
+    seed, top, treasury, fund, fund_id = 45, 1000, 1000, 1_000_000, 10**15
+    n_win, win = 2, 32
+    n_x = n_win * win * BM
+    gpu = StateMachine(batch_max=BM, accounts_max=N_ACC + treasury, transfers_max=n_x + N_ACC,
+                       window_events_max=128 * BM)
+    ref = OracleStateMachine(batch_max=BM)
+    try:
+        acc = _batches(workload.accounts_cfg3(0, N_ACC + treasury, seed, N_ACC, top))
+        for w0 in range(0, len(acc), 128):
+            assert commit_window(gpu, Operation.create_accounts, acc[w0:w0 + 128]) == \
+                oracle_batches(ref, Operation.create_accounts, acc[w0:w0 + 128])
+        fb = _batches(workload.funding_cfg3(0, N_ACC, seed, N_ACC, treasury, fund, fund_id))
+        for w0 in range(0, len(fb), 128):
+            assert commit_window(gpu, Operation.create_transfers, fb[w0:w0 + 128]) == \
+                oracle_batches(ref, Operation.create_transfers, fb[w0:w0 + 128])
+        host = workload.transfers_zipf(0, n_x, seed, N_ACC, workload.zipf_cdf(N_ACC))
+        fails = 0
+        for w in range(n_win):
+            xb = _batches(host, w * win * BM, win * BM)
+            g = commit_window(gpu, Operation.create_transfers, xb)
+            r = oracle_batches(ref, Operation.create_transfers, xb)
+            assert g == r, f"window {w}"
+            fails += sum(len(x) // 8 for x in r)
+        assert fails > 0  # exceeds_credits happens
+        assert gpu.stats()["resolver_events"] > 0
+        _check_digest(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_geometry_cfg5_g8_128_batch_windows():
+    """cfg5's protocol at G = 8 (hash shards on one GPU, exchanges summed in-process) with
+    128-batch windows: ~7/8 of the transfers cross-shard."""
+    from test_gpu_shard import LocalShards, _compare_sharded
+
+    G, seed, n_win = 8, 47, 2
+    n_x = n_win * 128 * BM
+    sh = LocalShards(G, BM, N_ACC // G + 65536, n_x // G + 128 * BM, 128 * BM)
+    ref = OracleStateMachine(batch_max=BM)
+    try:
+        acc = _batches(workload.accounts(0, N_ACC, seed))
+        for w0 in range(0, len(acc), 128):
+            assert sh.commit_window(Operation.create_accounts, acc[w0:w0 + 128]) == \
+                oracle_batches(ref, Operation.create_accounts, acc[w0:w0 + 128])
+        host = workload.transfers_uniform(0, n_x, seed, N_ACC)
+        for w in range(n_win):
+            xb = _batches(host, w * 128 * BM, 128 * BM)
+            assert sh.commit_window(Operation.create_transfers, xb) == \
+                oracle_batches(ref, Operation.create_transfers, xb)
+        _compare_sharded(sh, ref)
+    finally:
+        sh.close()
+        ref.close()
