@@ -103,6 +103,34 @@ typedef struct tb_transfer_pending_t {
     uint8_t padding[7];
 } tb_transfer_pending_t;
 
+/* AccountFilter (tigerbeetle.zig:288-322): the input of get_account_transfers and
+ * get_account_balances. 64 B. timestamp_min / timestamp_max 0 = unbounded (inclusive bounds). */
+typedef struct __attribute__((aligned(16))) tb_account_filter {
+    tb_uint128_t account_id; /*  0 */
+    uint64_t timestamp_min;  /* 16 */
+    uint64_t timestamp_max;  /* 24 */
+    uint32_t limit;          /* 32 */
+    uint32_t flags;          /* 36: TB_FILTER_* */
+    uint8_t reserved[24];    /* 40 */
+} tb_account_filter_t;
+
+/* AccountFilterFlags (tigerbeetle.zig:309-322). */
+enum {
+    TB_FILTER_DEBITS = 1u << 0,
+    TB_FILTER_CREDITS = 1u << 1,
+    TB_FILTER_REVERSED = 1u << 2
+};
+
+/* AccountBalance (tigerbeetle.zig:65-78): one row of get_account_balances. 128 B. */
+typedef struct __attribute__((aligned(16))) tb_account_balance {
+    tb_uint128_t debits_pending;  /*  0 */
+    tb_uint128_t debits_posted;   /* 16 */
+    tb_uint128_t credits_pending; /* 32 */
+    tb_uint128_t credits_posted;  /* 48 */
+    uint64_t timestamp;           /* 64 */
+    uint8_t reserved[56];         /* 72 */
+} tb_account_balance_t;
+
 /* Operation (state_machine.zig:341-350). */
 enum {
     TB_OP_PULSE = 128,
@@ -217,10 +245,14 @@ enum {
 static_assert(sizeof(tb_account_t) == 128, "Account is 128 B");
 static_assert(sizeof(tb_transfer_t) == 128, "Transfer is 128 B");
 static_assert(sizeof(tb_create_result_t) == 8, "Create*sResult is 8 B");
+static_assert(sizeof(tb_account_filter_t) == 64, "AccountFilter is 64 B");
+static_assert(sizeof(tb_account_balance_t) == 128, "AccountBalance is 128 B");
 #else
 _Static_assert(sizeof(tb_account_t) == 128, "Account is 128 B");
 _Static_assert(sizeof(tb_transfer_t) == 128, "Transfer is 128 B");
 _Static_assert(sizeof(tb_create_result_t) == 8, "Create*sResult is 8 B");
+_Static_assert(sizeof(tb_account_filter_t) == 64, "AccountFilter is 64 B");
+_Static_assert(sizeof(tb_account_balance_t) == 128, "AccountBalance is 128 B");
 #endif
 
 #endif /* TB_TYPES_H */

@@ -204,6 +204,11 @@ typedef struct tbo_state {
     uint64_t pulse_next_timestamp; /* ExpirePendingTransfers.pulse_next_timestamp (:2063) */
     uint32_t batch_max;            /* constants.batch_max.create_transfers (pulse cap, :1016-1022) */
     uint64_t commit_timestamp;
+    /* account_balances groove (state_machine.zig:296-315): one row per transfer record (same
+     * index, so the transfer insert's undo also drops it); hist_side bit 0 = dr side, bit 1 = cr */
+    tb_uint128_t (*hist)[8];
+    uint8_t *hist_side;
+    uint64_t hist_cap;
     /* scope */
     int scope_active;
     undo_rec *undo;
@@ -311,6 +316,12 @@ static void insert_transfer(tbo_state *s, const tb_transfer_t *t) {
         s->xfer = (tb_transfer_t *)realloc(s->xfer, s->xfer_cap * sizeof(tb_transfer_t));
     }
     s->xfer[s->xfer_n] = *t;
+    if (s->xfer_n >= s->hist_cap) {
+        s->hist_cap = s->xfer_cap;
+        s->hist = (tb_uint128_t(*)[8])realloc(s->hist, s->hist_cap * sizeof(*s->hist));
+        s->hist_side = (uint8_t *)realloc(s->hist_side, s->hist_cap);
+    }
+    s->hist_side[s->xfer_n] = 0;
     omap_put(&s->xfer_map, t->id, (uint32_t)s->xfer_n);
     s->xfer_n++;
     undo_rec r = {0};
@@ -322,6 +333,29 @@ static void insert_transfer(tbo_state *s, const tb_transfer_t *t) {
         xentry e = {t->timestamp + (uint64_t)t->timeout * TB_NS_PER_S, t->timestamp};
         xheap_push(&s->xh, e);
     }
+}
+
+/* historical_balance (state_machine.zig:1806-1841): the row of the transfer just inserted (the
+ * last record), with each history account's balances after the transfer. */
+static void historical_balance(tbo_state *s, const tb_account_t *dr, const tb_account_t *cr) {
+    if (!((dr->flags | cr->flags) & TB_ACCOUNT_HISTORY)) return;
+    const uint64_t i = s->xfer_n - 1;
+    uint8_t side = 0;
+    if (dr->flags & TB_ACCOUNT_HISTORY) {
+        side |= 1;
+        s->hist[i][0] = dr->debits_pending;
+        s->hist[i][1] = dr->debits_posted;
+        s->hist[i][2] = dr->credits_pending;
+        s->hist[i][3] = dr->credits_posted;
+    }
+    if (cr->flags & TB_ACCOUNT_HISTORY) {
+        side |= 2;
+        s->hist[i][4] = cr->debits_pending;
+        s->hist[i][5] = cr->debits_posted;
+        s->hist[i][6] = cr->credits_pending;
+        s->hist[i][7] = cr->credits_posted;
+    }
+    s->hist_side[i] = side;
 }
 
 static void insert_pending(tbo_state *s, uint64_t ts, uint8_t status) {
@@ -509,6 +543,7 @@ static uint32_t post_or_void_pending_transfer(tbo_state *s, const tb_transfer_t 
     }
     update_account(s, dr, dp, dpo, U(dr->credits_pending), U(dr->credits_posted));
     update_account(s, cr, U(cr->debits_pending), U(cr->debits_posted), ccp, cpo);
+    historical_balance(s, dr, cr); /* :1732-1736 */
     s->commit_timestamp = t->timestamp;
     return TB_CT_OK;
 }
@@ -593,7 +628,7 @@ static uint32_t create_transfer(tbo_state *s, const tb_transfer_t *t) {
         update_account(s, dr, dr_dp, dr_dpo + amount, dr_cp, dr_cpo);
         update_account(s, cr, cr_dp, cr_dpo, cr_cp, cr_cpo + amount);
     }
-    /* historical_balance (:1806-1841) only feeds get_account_balances (out of scope). */
+    historical_balance(s, dr, cr); /* :1570-1574 */
     if (t->timeout > 0) {
         const uint64_t expires_at = t->timestamp + (uint64_t)t->timeout * TB_NS_PER_S;
         if (expires_at < s->pulse_next_timestamp) s->pulse_next_timestamp = expires_at;
@@ -748,6 +783,8 @@ void tbo_destroy(tbo_state *s) {
     free(s->pend_xfer);
     free(s->xh.a);
     free(s->undo);
+    free(s->hist);
+    free(s->hist_side);
     free(s);
 }
 
@@ -838,4 +875,80 @@ uint64_t tbo_dump_transfer_status(tbo_state *s, uint8_t *out, uint64_t cap) {
         out[i] = slot < 0 ? 0 : s->pend_status[slot];
     }
     return n;
+}
+
+/* ----------------------------------------------------------------------------------------------
+ * get_account_transfers / get_account_balances (state_machine.zig:786-996, 1346-1419). The
+ * reference scans the transfers groove's debit_account_id / credit_account_id indexes (a union of
+ * the two when both flags are set) over the timestamp range, ascending or descending, into a buffer
+ * of min(limit, batch_max) results; an invalid filter (get_scan_from_filter, :931-944) or, for
+ * balances, a missing account or one without flags.history gives an empty reply. Records are kept
+ * in timestamp order, so the scan is a filtered walk over them.
+ * -------------------------------------------------------------------------------------------- */
+static int filter_valid(const tb_account_filter_t *f) {
+    const u128 id = U(f->account_id);
+    if (id == 0 || id == MAX128) return 0;
+    if (f->timestamp_min == UINT64_MAX || f->timestamp_max == UINT64_MAX) return 0;
+    if (f->timestamp_max != 0 && f->timestamp_min > f->timestamp_max) return 0;
+    if (f->limit == 0) return 0;
+    if (!(f->flags & (TB_FILTER_DEBITS | TB_FILTER_CREDITS))) return 0;
+    if (f->flags & ~(uint32_t)(TB_FILTER_DEBITS | TB_FILTER_CREDITS | TB_FILTER_REVERSED)) return 0;
+    for (int k = 0; k < 24; k++)
+        if (f->reserved[k]) return 0;
+    return 1;
+}
+
+/* Indexes of the matching transfer records, in scan order, at most `cap`. */
+static uint32_t account_scan(const tbo_state *s, const tb_account_filter_t *f, uint32_t cap, uint32_t *idx) {
+    const uint64_t tmin = f->timestamp_min ? f->timestamp_min : TB_TIMESTAMP_MIN;
+    const uint64_t tmax = f->timestamp_max ? f->timestamp_max : TB_TIMESTAMP_MAX;
+    const int rev = (f->flags & TB_FILTER_REVERSED) != 0;
+    uint32_t n = 0;
+    for (uint64_t k = 0; k < s->xfer_n && n < cap; k++) {
+        const uint64_t i = rev ? s->xfer_n - 1 - k : k;
+        const tb_transfer_t *t = &s->xfer[i];
+        if (t->timestamp < tmin || t->timestamp > tmax) continue;
+        const int dr = (f->flags & TB_FILTER_DEBITS) && U(t->debit_account_id) == U(f->account_id);
+        const int cr = (f->flags & TB_FILTER_CREDITS) && U(t->credit_account_id) == U(f->account_id);
+        if (dr || cr) idx[n++] = (uint32_t)i;
+    }
+    return n;
+}
+
+uint32_t tbo_get_account_transfers(tbo_state *s, const tb_account_filter_t *f, tb_transfer_t *out) {
+    if (!filter_valid(f)) return 0;
+    const uint32_t cap = f->limit < s->batch_max ? f->limit : s->batch_max;
+    uint32_t *idx = (uint32_t *)malloc((size_t)cap * sizeof(uint32_t));
+    const uint32_t n = account_scan(s, f, cap, idx);
+    for (uint32_t k = 0; k < n; k++) out[k] = s->xfer[idx[k]];
+    free(idx);
+    return n;
+}
+
+uint32_t tbo_get_account_balances(tbo_state *s, const tb_account_filter_t *f, tb_account_balance_t *out) {
+    const tb_account_t *a = get_account(s, f->account_id);
+    if (!a || !(a->flags & TB_ACCOUNT_HISTORY) || !filter_valid(f)) return 0;
+    const uint32_t cap = f->limit < s->batch_max ? f->limit : s->batch_max;
+    uint32_t *idx = (uint32_t *)malloc((size_t)cap * sizeof(uint32_t));
+    const uint32_t n = account_scan(s, f, cap, idx);
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t i = idx[k];
+        const tb_transfer_t *t = &s->xfer[i];
+        /* the side of the queried account (execute_get_account_balances, :1392-1410); a record
+         * without its row (the expired post/void quirk) is skipped: the reference would reach
+         * `unreachable` in its scan lookup (lsm/scan_lookup.zig) */
+        int side = U(t->debit_account_id) == U(f->account_id) ? 0 : 1;
+        if (!(s->hist_side[i] & (1u << side))) continue;
+        tb_account_balance_t b;
+        memset(&b, 0, sizeof b);
+        b.debits_pending = s->hist[i][4 * side + 0];
+        b.debits_posted = s->hist[i][4 * side + 1];
+        b.credits_pending = s->hist[i][4 * side + 2];
+        b.credits_posted = s->hist[i][4 * side + 3];
+        b.timestamp = t->timestamp;
+        out[c++] = b;
+    }
+    free(idx);
+    return c;
 }

@@ -5,7 +5,8 @@ Run once in the build container (the reference tree is not present on the GPU bo
     python tests/golden/extract_kats.py /root/reference/src/state_machine.zig
 
 Each `try check(<table>)` block of a test in the in-scope range (create_accounts, linked chains,
-create_transfers, two-phase, expiry, chain rollback, balancing: state_machine.zig:2767-3360) is
+create_transfers, two-phase, expiry, chain rollback, balancing, and the
+get_account_transfers / get_account_balances queries: state_machine.zig:2767-3571) is
 written verbatim as data to tests/golden/kat_<test-name>[_<k>].tbl, with a header naming the
 source lines. The rows are inputs and expected outputs only (events, expected result codes,
 expected balances); they are parsed by tests/kat.py, which mirrors testing/table.zig:8-93 and the
@@ -15,7 +16,7 @@ import os
 import re
 import sys
 
-IN_SCOPE = (2767, 3360)
+IN_SCOPE = (2767, 3571)
 
 
 def main(path):

@@ -18,6 +18,11 @@ import numpy as np
 
 from tigerbeetle_amd.types import (
     ACCOUNT_DTYPE,
+    BALANCE_DTYPE,
+    FILTER_CREDITS,
+    FILTER_DEBITS,
+    FILTER_DTYPE,
+    FILTER_REVERSED,
     RESULT_DTYPE,
     TRANSFER_DTYPE,
     U64_MAX,
@@ -52,6 +57,15 @@ TRANSFER_COLUMNS = [
     ("result", ("enum", CreateTransferResult), None),
 ]  # TestCreateTransfer, state_machine.zig:2394-2441
 
+RESULT_TRANSFER_COLUMNS = TRANSFER_COLUMNS[:-1]  # TestGetAccountTransfersResult, state_machine.zig:2459-2500
+
+FILTER_COLUMNS = [
+    ("account_id", 128, None), ("timestamp_min_transfer_id", ("nint", 128), None),
+    ("timestamp_max_transfer_id", ("nint", 128), None), ("limit", 32, None),
+    ("flags_debits", ("opt", "DR"), None), ("flags_credits", ("opt", "CR"), None),
+    ("flags_reversed", ("opt", "REV"), None),
+]  # TestAccountFilter, state_machine.zig:2443-2457
+
 REQUIRED = object()
 
 
@@ -66,7 +80,7 @@ def _int(token, bits):
 def _parse_struct(columns, tokens):
     row = {}
     for name, kind, default in columns:
-        has_default = not (default is None and not (isinstance(kind, tuple) and kind[0] == "opt"))
+        has_default = not (default is None and not (isinstance(kind, tuple) and kind[0] in ("opt", "nint")))
         if has_default and tokens and tokens[0] == "_":
             tokens.pop(0)
             row[name] = default
@@ -77,6 +91,8 @@ def _parse_struct(columns, tokens):
         elif kind[0] == "opt":
             assert tok == kind[1], (name, tok)
             row[name] = True
+        elif kind[0] == "nint":  # an optional integer: `_` = null
+            row[name] = _int(tok, kind[1])
         elif kind[0] == "enum":
             row[name] = kind[1][tok]
     return row
@@ -127,6 +143,12 @@ def parse(table):
                 assert variant == "amount"
                 val = _int(tok, 128)
             actions.append(("lookup_transfer", (ident, variant, val)))
+        elif kind in ("get_account_transfers", "get_account_balances"):
+            actions.append((kind, _parse_struct(FILTER_COLUMNS, tokens)))
+        elif kind == "get_account_transfers_result":
+            actions.append((kind, _parse_struct(RESULT_TRANSFER_COLUMNS, tokens)))
+        elif kind == "get_account_balances_result":
+            actions.append((kind, [_int(tokens.pop(0), 128) for _ in range(5)]))
         else:
             raise ValueError("unsupported row: " + line)
         assert not tokens, ("trailing tokens", line, tokens)
@@ -240,6 +262,30 @@ def check(sm, table):
                 rec = transfers[ident].copy()
                 set_u128(rec[0], "amount", val)
                 reply.append(rec.tobytes())
+        elif action in ("get_account_transfers", "get_account_balances"):
+            # state_machine.zig:2648-2700: timestamp bounds name a transfer whose timestamp they take
+            op_q = Operation[action]
+            assert operation in (None, op_q)
+            operation = op_q
+            f = np.zeros(1, FILTER_DTYPE)
+            set_u128(f[0], "account_id", p["account_id"])
+            for key, col in (("timestamp_min_transfer_id", "timestamp_min"),
+                             ("timestamp_max_transfer_id", "timestamp_max")):
+                f[0][col] = 0 if p[key] is None else int(transfers[p[key]][0]["timestamp"])
+            f[0]["limit"] = p["limit"]
+            f[0]["flags"] = ((FILTER_DEBITS if p["flags_debits"] else 0) | (FILTER_CREDITS if p["flags_credits"] else 0)
+                             | (FILTER_REVERSED if p["flags_reversed"] else 0))
+            request.append(f.tobytes())
+        elif action == "get_account_transfers_result":
+            assert operation == Operation.get_account_transfers
+            reply.append(transfer_record(p, int(transfers[p["id"]][0]["timestamp"])).tobytes())
+        elif action == "get_account_balances_result":
+            assert operation == Operation.get_account_balances
+            b = np.zeros(1, BALANCE_DTYPE)
+            for f_, v in zip(("debits_pending", "debits_posted", "credits_pending", "credits_posted"), p[1:]):
+                set_u128(b[0], f_, v)
+            b[0]["timestamp"] = transfers[p[0]][0]["timestamp"]
+            reply.append(b.tobytes())
         elif action == "commit":
             assert operation in (None, p)
             req = b"".join(request)
@@ -265,7 +311,8 @@ def _diff(operation, expected, actual):
         e = np.frombuffer(expected, RESULT_DTYPE).tolist()
         a = np.frombuffer(actual, RESULT_DTYPE).tolist()
         return f"{operation.name}: expected {e}\n actual {a}"
-    dt = ACCOUNT_DTYPE if operation == Operation.lookup_accounts else TRANSFER_DTYPE
+    dt = {Operation.lookup_accounts: ACCOUNT_DTYPE, Operation.get_account_balances: BALANCE_DTYPE}.get(
+        operation, TRANSFER_DTYPE)
     e = np.frombuffer(expected, dt)
     a = np.frombuffer(actual, dt)
     return f"{operation.name}: expected {len(e)} records\n{e}\n actual {len(a)} records\n{a}"

@@ -10,7 +10,7 @@ import subprocess
 
 import numpy as np
 
-from tigerbeetle_amd.types import ACCOUNT_DTYPE, BATCH_MAX, RESULT_DTYPE, TRANSFER_DTYPE, Operation
+from tigerbeetle_amd.types import ACCOUNT_DTYPE, BALANCE_DTYPE, BATCH_MAX, RESULT_DTYPE, TRANSFER_DTYPE, Operation
 
 ORACLE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
 _lib = None
@@ -58,6 +58,9 @@ def lib():
         L.tbo_pending_status.argtypes = [vp, u64]
         L.tbo_pending_status.restype = u32
         L.tbo_input_valid.argtypes = [u32, u64, u32]
+        for f in (L.tbo_get_account_transfers, L.tbo_get_account_balances):
+            f.argtypes = [vp, vp, vp]
+            f.restype = u32
         L.tbo_dump_transfer_status.argtypes = [vp, vp, u64]
         L.tbo_dump_transfer_status.restype = u64
         _lib = L
@@ -113,6 +116,14 @@ class OracleStateMachine:
             out = np.zeros(max(n, 1), dt)
             fn = L.tbo_lookup_accounts if operation == Operation.lookup_accounts else L.tbo_lookup_transfers
             c = fn(self.h, buf.ctypes.data, n, out.ctypes.data)
+            return out[:c].tobytes()
+        if operation in (Operation.get_account_transfers, Operation.get_account_balances):
+            # input_valid (state_machine.zig:548-552) admits exactly one 64 B AccountFilter
+            out = np.zeros(self.batch_max, TRANSFER_DTYPE if operation == Operation.get_account_transfers
+                           else BALANCE_DTYPE)
+            fn = (L.tbo_get_account_transfers if operation == Operation.get_account_transfers
+                  else L.tbo_get_account_balances)
+            c = fn(self.h, buf.ctypes.data, out.ctypes.data)
             return out[:c].tobytes()
         raise NotImplementedError(operation)
 

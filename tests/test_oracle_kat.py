@@ -15,7 +15,7 @@ KAT_BATCH_MAX = 64
 
 
 def test_kat_inventory():
-    assert len(KATS) == 19
+    assert len(KATS) == 25
 
 
 @pytest.mark.parametrize("path", KATS, ids=[os.path.basename(p)[4:-4] for p in KATS])

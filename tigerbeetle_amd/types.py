@@ -33,7 +33,14 @@ TRANSFER_DTYPE = np.dtype(
        ("code", "<u2"), ("flags", "<u2"), ("timestamp", "<u8")]
 )
 RESULT_DTYPE = np.dtype([("index", "<u4"), ("result", "<u4")])
+# AccountFilter (tigerbeetle.zig:288-322) and AccountBalance (:65-78)
+FILTER_DTYPE = np.dtype(_u128("account_id") + [("timestamp_min", "<u8"), ("timestamp_max", "<u8"),
+                                               ("limit", "<u4"), ("flags", "<u4"), ("reserved", "u1", (24,))])
+BALANCE_DTYPE = np.dtype(_u128("debits_pending") + _u128("debits_posted") + _u128("credits_pending")
+                         + _u128("credits_posted") + [("timestamp", "<u8"), ("reserved", "u1", (56,))])
+FILTER_DEBITS, FILTER_CREDITS, FILTER_REVERSED = 1, 2, 4
 assert ACCOUNT_DTYPE.itemsize == 128 and TRANSFER_DTYPE.itemsize == 128 and RESULT_DTYPE.itemsize == 8
+assert FILTER_DTYPE.itemsize == 64 and BALANCE_DTYPE.itemsize == 128
 
 
 def set_u128(rec, name, value):
