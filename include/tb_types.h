@@ -131,6 +131,24 @@ typedef struct __attribute__((aligned(16))) tb_account_balance {
     uint8_t reserved[56];         /* 72 */
 } tb_account_balance_t;
 
+/* AccountBalancesGrooveValue (state_machine.zig:296-315): the account_balances groove row that
+ * historical_balance (:1806-1841) inserts, keyed by the transfer's timestamp; a side's account id is
+ * 0 when that account has no flags.history. 256 B. */
+typedef struct __attribute__((aligned(16))) tb_account_balances_value {
+    tb_uint128_t dr_account_id;      /*   0 */
+    tb_uint128_t dr_debits_pending;  /*  16 */
+    tb_uint128_t dr_debits_posted;   /*  32 */
+    tb_uint128_t dr_credits_pending; /*  48 */
+    tb_uint128_t dr_credits_posted;  /*  64 */
+    tb_uint128_t cr_account_id;      /*  80 */
+    tb_uint128_t cr_debits_pending;  /*  96 */
+    tb_uint128_t cr_debits_posted;   /* 112 */
+    tb_uint128_t cr_credits_pending; /* 128 */
+    tb_uint128_t cr_credits_posted;  /* 144 */
+    uint64_t timestamp;              /* 160 */
+    uint8_t reserved[88];            /* 168 */
+} tb_account_balances_value_t;
+
 /* Operation (state_machine.zig:341-350). */
 enum {
     TB_OP_PULSE = 128,
@@ -247,12 +265,14 @@ static_assert(sizeof(tb_transfer_t) == 128, "Transfer is 128 B");
 static_assert(sizeof(tb_create_result_t) == 8, "Create*sResult is 8 B");
 static_assert(sizeof(tb_account_filter_t) == 64, "AccountFilter is 64 B");
 static_assert(sizeof(tb_account_balance_t) == 128, "AccountBalance is 128 B");
+static_assert(sizeof(tb_account_balances_value_t) == 256, "AccountBalancesGrooveValue is 256 B");
 #else
 _Static_assert(sizeof(tb_account_t) == 128, "Account is 128 B");
 _Static_assert(sizeof(tb_transfer_t) == 128, "Transfer is 128 B");
 _Static_assert(sizeof(tb_create_result_t) == 8, "Create*sResult is 8 B");
 _Static_assert(sizeof(tb_account_filter_t) == 64, "AccountFilter is 64 B");
 _Static_assert(sizeof(tb_account_balance_t) == 128, "AccountBalance is 128 B");
+_Static_assert(sizeof(tb_account_balances_value_t) == 256, "AccountBalancesGrooveValue is 256 B");
 #endif
 
 #endif /* TB_TYPES_H */

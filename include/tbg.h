@@ -77,10 +77,12 @@ int tbg_pulse_needed(tbg_engine *engine, uint64_t prepare_timestamp, int *needed
 int tbg_prefetch(tbg_engine *engine, uint64_t op, uint32_t operation, const void *input, uint64_t input_len,
                  uint64_t prefetch_timestamp);
 
-/* StateMachine.commit (state_machine.zig:1107-1146) for pulse, create_accounts, create_transfers,
- * lookup_accounts and lookup_transfers. Writes exactly the reply bytes the reference writes into
- * `output` (for create_*: packed {u32 index, u32 result} for non-ok events, ascending index) and
- * the byte count into *output_len. Synchronous. */
+/* StateMachine.commit (state_machine.zig:1107-1146) for every operation: pulse, create_accounts,
+ * create_transfers, lookup_accounts, lookup_transfers, get_account_transfers and
+ * get_account_balances (input: one tb_account_filter_t; reply: Transfer / AccountBalance records,
+ * :1346-1419). Writes exactly the reply bytes the reference writes into `output` (for create_*:
+ * packed {u32 index, u32 result} for non-ok events, ascending index) and the byte count into
+ * *output_len. Synchronous. Queries run on unsharded engines (TBG_E_STATE on a shard). */
 int tbg_commit(tbg_engine *engine, uint64_t op, uint64_t timestamp, uint32_t operation, const void *input,
                uint64_t input_len, void *output, uint64_t output_cap, uint64_t *output_len);
 
@@ -149,10 +151,12 @@ int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, const vo
 /* StateMachine.open (state_machine.zig:527-541), after a restart or a state sync: an empty engine
  * takes the LSM forest's objects: every Account and every Transfer in timestamp order (the grooves'
  * object trees are keyed by timestamp) and, per transfer, its TransferPending status (0 none,
- * 1 pending, 2 posted, 3 voided, 4 expired; NULL = all 0). pulse_next_timestamp starts at
+ * 1 pending, 2 posted, 3 voided, 4 expired; NULL = all 0), and the account_balances groove's rows
+ * (historical_balance, :1806-1841; sorted by timestamp). pulse_next_timestamp starts at
  * timestamp_min, as in a freshly initialised StateMachine (:2063). TBG_E_STATE if not empty. */
 int tbg_open(tbg_engine *engine, const tb_account_t *accounts, uint64_t n_accounts, const tb_transfer_t *transfers,
-             uint64_t n_transfers, const uint8_t *pending_status);
+             uint64_t n_transfers, const uint8_t *pending_status,
+             const tb_account_balances_value_t *account_balances, uint64_t n_account_balances);
 /* StateMachine.reset (state_machine.zig:486-501): back to an empty state machine. */
 int tbg_reset(tbg_engine *engine);
 /* Prefetch completion (state_machine.zig:598-648 completes through a callback, possibly on the next

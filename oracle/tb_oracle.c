@@ -952,3 +952,36 @@ uint32_t tbo_get_account_balances(tbo_state *s, const tb_account_filter_t *f, tb
     free(idx);
     return c;
 }
+
+/* The account_balances groove's rows (state_machine.zig:296-315) in timestamp order: what a forest
+ * hands to StateMachine.open. Returns the row count (rows written up to cap). */
+uint64_t tbo_dump_account_balances(const tbo_state *s, tb_account_balances_value_t *out, uint64_t cap) {
+    uint64_t n = 0;
+    for (uint64_t i = 0; i < s->xfer_n; i++) {
+        const uint8_t side = s->hist_side[i];
+        if (!side) continue;
+        if (n < cap) {
+            tb_account_balances_value_t r;
+            memset(&r, 0, sizeof r);
+            const tb_transfer_t *t = &s->xfer[i];
+            if (side & 1) {
+                r.dr_account_id = t->debit_account_id;
+                r.dr_debits_pending = s->hist[i][0];
+                r.dr_debits_posted = s->hist[i][1];
+                r.dr_credits_pending = s->hist[i][2];
+                r.dr_credits_posted = s->hist[i][3];
+            }
+            if (side & 2) {
+                r.cr_account_id = t->credit_account_id;
+                r.cr_debits_pending = s->hist[i][4];
+                r.cr_debits_posted = s->hist[i][5];
+                r.cr_credits_pending = s->hist[i][6];
+                r.cr_credits_posted = s->hist[i][7];
+            }
+            r.timestamp = t->timestamp;
+            out[n] = r;
+        }
+        n++;
+    }
+    return n;
+}

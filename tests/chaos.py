@@ -21,13 +21,13 @@ def _pick(rng, choices):
 
 class Chaos:
     def __init__(self, seed, n_accounts=40, id_space=400, huge=False, limits=0.3, linked=0.15, pending=0.3,
-                 postvoid=0.25, balancing=0.08, invalid=0.05):
+                 postvoid=0.25, balancing=0.08, invalid=0.05, history=0.0):
         self.rng = random.Random(seed)
         self.n_accounts = n_accounts
         self.id_space = id_space
         self.huge = huge
         self.p = dict(limits=limits, linked=linked, pending=pending, postvoid=postvoid, balancing=balancing,
-                      invalid=invalid)
+                      invalid=invalid, history=history)
         self.pending_ids = []
         self.history = []  # recent transfer events, for idempotent retries
 
@@ -46,6 +46,8 @@ class Chaos:
                 f |= 1
             if rng.random() < 0.02:
                 f |= 6  # mutually exclusive
+            if self.p["history"] and rng.random() < self.p["history"]:
+                f |= 8  # flags.history: historical_balance rows (get_account_balances)
             a[i]["flags"] = f
             a[i]["user_data_64"] = rng.randint(0, 2)
             if rng.random() < self.p["invalid"]:

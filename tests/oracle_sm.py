@@ -61,6 +61,8 @@ def lib():
         for f in (L.tbo_get_account_transfers, L.tbo_get_account_balances):
             f.argtypes = [vp, vp, vp]
             f.restype = u32
+        L.tbo_dump_account_balances.argtypes = [vp, vp, u64]
+        L.tbo_dump_account_balances.restype = u64
         L.tbo_dump_transfer_status.argtypes = [vp, vp, u64]
         L.tbo_dump_transfer_status.restype = u64
         _lib = L
@@ -155,3 +157,11 @@ class OracleStateMachine:
         out = np.zeros(max(n, 1), np.uint8)
         L.tbo_dump_transfer_status(self.h, out.ctypes.data, n)
         return out[:n]
+
+    def dump_account_balances(self):
+        """The account_balances groove's rows, timestamp order (256 B each)."""
+        L = lib()
+        n = L.tbo_dump_account_balances(self.h, None, 0)
+        out = np.zeros(max(n, 1) * 256, np.uint8)
+        L.tbo_dump_account_balances(self.h, out.ctypes.data, n)
+        return out[: n * 256]

@@ -106,7 +106,7 @@ def lib():
         "tbg_window_changes": ([vp, vp, u64, P(u64), vp, u64, P(u64), vp, u64, P(u64)], i32),
         "tbg_shard_exchange_bytes": ([u32, u32], u64),
         "tbg_windows_committed": ([vp, P(u64), P(u64)], i32),
-        "tbg_open": ([vp, vp, u64, vp, u64, vp], i32),
+        "tbg_open": ([vp, vp, u64, vp, u64, vp, vp, u64], i32),
         "tbg_reset": ([vp], i32),
         "tbg_prefetch_poll": ([vp, P(ctypes.c_int)], i32),
         "tbg_compact": ([vp, u64], i32),

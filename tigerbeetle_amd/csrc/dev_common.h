@@ -172,6 +172,8 @@ enum : uint32_t {
                            // a post/void of a pending transfer with a timeout (state_machine.zig:1576-1581,
                            // 1704-1708); applies if the event ran ok, even if its chain is rolled back
   C_RANOK = 1u << 20,      // ran ok, then rolled back with its chain (code back-filled linked_event_failed)
+  C_HIST = 1u << 21,       // touches an account with flags.history: its history row needs the balances
+                           // after it in order, so it runs on the sequential walker
 };
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

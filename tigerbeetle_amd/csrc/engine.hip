@@ -43,6 +43,7 @@
 #include "window.h"
 #include "changes.h"
 #include "restore.h"
+#include "query.h"
 
 // k_final's streams, nontemporal: the window's event records (read for the last time) and the
 // inserted transfer records pass by, while the account table and records stay cached across windows
@@ -190,6 +191,9 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
               AccEntry de, ce;
               dr_slot = acc_find(d.acc_tab, d.acc_mask, p.debit_account_id, &de);
               cr_slot = acc_find(d.acc_tab, d.acc_mask, p.credit_account_id, &ce);
+              if ((dr_slot != NONE32 && (de.flags & TB_ACCOUNT_HISTORY)) ||
+                  (cr_slot != NONE32 && (ce.flags & TB_ACCOUNT_HISTORY)))
+                cls |= C_HIST;
             }
             if (code == CONT && id_tslot != NONE32) code = pv_exists(t, d.xr[id_tslot], p);
             if (code == CONT) code = pv_status(d.xstatus[p_tslot]);
@@ -227,6 +231,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
             cls |= C_STATIC;
           } else {
             cls |= C_REACH;
+            if ((de.flags | ce.flags) & TB_ACCOUNT_HISTORY) cls |= C_HIST;
             id_ent = spec ? bmap_direct(s.bmap, s.bmask, i, epoch) : bmap_claim(s.bmap, s.bmask, evb, t.id, i, 0, epoch);
             const bool bal = f & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT);
             amount_upper = U(t.amount);
@@ -267,6 +272,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
       s.pnv[i] = pnv;
       atomicOr(&aux, 8u);
     }
+    if (cls & C_HIST) atomicOr(&aux, 32u);
     // Hot marks: the first marker of an account this window gives it the next dense rank.
     if (cls & C_READS_DR) mark_hot(d, dr_slot, epoch);
     if (cls & C_READS_CR) mark_hot(d, cr_slot, epoch);
@@ -331,7 +337,9 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
     const bool prefix = claim_free && (aux & 4u) && g->x_sorted == g->x_count;
     // bit 2: pulse_next ops; bit 3: a post/void that may reset pulse_next (k_final replays the
     // window's ops in order only then; else pulse_next = min(itself, the creations that ran ok))
-    g->win_flags = (claim_free ? 1u : 0u) | (prefix ? 2u : 0u) | ((aux & 8u) ? 4u : 0u) | ((aux & 16u) ? 8u : 0u);
+    // bit 4: history rows: the sequential walker (exact balances after each event) decides W
+    g->win_flags = (claim_free ? 1u : 0u) | (prefix ? 2u : 0u) | ((aux & 8u) ? 4u : 0u) | ((aux & 16u) ? 8u : 0u) |
+                   ((aux & 32u) ? 16u : 0u);
     // every balance field stays below 2^64 this window (k_walk computes the same for k_final; the
     // component walkers, which run before k_walk, read it from here)
     const u128 sum = g->ovf_bound + g->batch_amount_sum;
@@ -415,7 +423,7 @@ __device__ inline bool is_u(const Scratch& s, uint32_t j, uint32_t cls, uint32_t
                             bool claim_free) {
   if (!(cls & C_REACH)) return false;
   if (!XFER) return bmap_idc(s.bmap, s.id_ent[j], epoch) > 1;  // duplicate account id in the window
-  if (ovf_mode || (cls & (C_READS_DR | C_READS_CR))) return true;
+  if (ovf_mode || (cls & (C_READS_DR | C_READS_CR | C_HIST))) return true;
   if (claim_free) return false;  // no id repeats and no post/void in the window (k_prep_reduce)
   const uint32_t e = s.id_ent[j];
   // duplicate transfer id, or a post/void in the window targets this id
@@ -443,7 +451,7 @@ __device__ inline bool is_w(const Dev& d, const Scratch& s, uint32_t j, uint32_t
 
 // A W event outside the resolver's class (resolver.h) sends the whole window to the walker.
 __device__ inline bool res_bad(const Scratch& s, uint32_t j, uint32_t cls, uint32_t epoch) {
-  if (cls & (C_LINKED | C_POSTVOID | C_BAL)) return true;
+  if (cls & (C_LINKED | C_POSTVOID | C_BAL | C_HIST)) return true;
   if (!(cls & C_REACH)) return false;
   const uint32_t e = s.id_ent[j];
   return bmap_idc(s.bmap, e, epoch) > 1 || bmap_pidc(s.bmap, e, epoch) > 0;
@@ -998,6 +1006,10 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
         if (!wev) {
           rw_stamp(rec, win_ts(w, b, i));
           if (cls & C_POSTVOID) rw_post_void(rec, &d.xr[s.p_tslot[i]], s.amt[i]);
+        }
+        if (wev && s.hside[i]) {  // historical_balance row (the walker computed it)
+          d.hist[slot] = s.hrow[i];
+          d.hist_side[slot] = s.hside[i];
         }
         // records of a prefix-extending window are found by binary search (x_prefix_find)
         if (!(TBG_EXPERIMENTS && (o.xskip & 2)) && !prefix_win) x_insert(d.x_tab, d.x_mask, rw_u128(rec[0]), (uint32_t)slot);

@@ -54,6 +54,28 @@ __global__ void __launch_bounds__(256) k_load_transfers(Dev d, uint64_t first, u
   }
 }
 
+// The account_balances groove's rows (sorted by timestamp): each lands on the slot of the transfer
+// with its timestamp (binary search over the timestamp-ordered store).
+__global__ void __launch_bounds__(256) k_load_history(Dev d, const tb_account_balances_value_t* rows, uint64_t n,
+                                                      uint64_t n_x) {
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    const tb_account_balances_value_t r = rows[k];
+    uint64_t a = 0, b = n_x;
+    while (a < b) {
+      const uint64_t m = (a + b) >> 1;
+      if (d.xr[m].timestamp < r.timestamp) a = m + 1; else b = m;
+    }
+    if (a >= n_x || d.xr[a].timestamp != r.timestamp) continue;  // no such transfer: not a row of ours
+    HistRow h;
+    h.dr[0] = U(r.dr_debits_pending), h.dr[1] = U(r.dr_debits_posted);
+    h.dr[2] = U(r.dr_credits_pending), h.dr[3] = U(r.dr_credits_posted);
+    h.cr[0] = U(r.cr_debits_pending), h.cr[1] = U(r.cr_debits_posted);
+    h.cr[2] = U(r.cr_credits_pending), h.cr[3] = U(r.cr_credits_posted);
+    d.hist[a] = h;
+    d.hist_side[a] = (U(r.dr_account_id) != 0 ? 1u : 0u) | (U(r.cr_account_id) != 0 ? 2u : 0u);
+  }
+}
+
 __global__ void k_load_finish(Dev d, const LoadBound* lb, uint64_t n_acc, uint64_t n_x) {
   Globals* g = d.g;
   g->acc_count = n_acc;

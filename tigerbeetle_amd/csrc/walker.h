@@ -140,8 +140,29 @@ struct Walker {
     }
   }
 
+  // historical_balance (:1806-1841): the row of event i from the accounts' balances after it
+  // (sequential mode only: windows with history accounts never run component walkers)
+  __device__ void history(uint32_t i, uint32_t drs, const Bal& dr, uint32_t crs, const Bal& cr) {
+    const uint16_t fd = d.acc[drs].flags, fc = d.acc[crs].flags;
+    if (!((fd | fc) & TB_ACCOUNT_HISTORY)) return;
+    HistRow r;
+    uint8_t side = 0;
+    for (int k = 0; k < 4; k++) r.dr[k] = r.cr[k] = 0;
+    if (fd & TB_ACCOUNT_HISTORY) {
+      side |= 1;
+      r.dr[0] = dr.dp, r.dr[1] = dr.dpo, r.dr[2] = dr.cp, r.dr[3] = dr.cpo;
+    }
+    if (fc & TB_ACCOUNT_HISTORY) {
+      side |= 2;
+      r.cr[0] = cr.dp, r.cr[1] = cr.dpo, r.cr[2] = cr.cp, r.cr[3] = cr.cpo;
+    }
+    s.hrow[i] = r;
+    s.hside[i] = side;
+  }
+
   __device__ void commit_record(uint32_t i, const tb_transfer_t& t2) {
     s.t2[i] = t2;
+    s.hside[i] = 0;
     log_small(UNDO_INS, i, 0);
     s.ins[i] = 1;
     const uint32_t e = s.id_ent[i];
@@ -186,6 +207,7 @@ struct Walker {
     }
     store_bal(dra, dr);
     store_bal(cra, cr);
+    history(i, drs, dr, crs, cr);  // :1570-1574
     return TB_CT_OK;
   }
 
@@ -257,6 +279,7 @@ struct Walker {
     }
     store_bal(dra, dr);
     store_bal(cra, cr);
+    history(i, drs, dr, crs, cr);  // :1732-1736
     return TB_CT_OK;
   }
 

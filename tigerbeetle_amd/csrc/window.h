@@ -39,6 +39,15 @@ struct __attribute__((aligned(16))) UndoRec {
   u128 old[4];
 };
 
+// account_balances groove row (state_machine.zig:296-315) of one transfer, beside its record: the
+// dr and cr accounts' balances after the transfer (historical_balance, :1806-1841); Dev::hist_side
+// says which sides are present (bit 0 dr, bit 1 cr: the accounts with flags.history).
+struct HistRow {
+  u128 dr[4];  // debits_pending, debits_posted, credits_pending, credits_posted
+  u128 cr[4];
+};
+static_assert(sizeof(HistRow) == 128, "HistRow");
+
 struct Dev {
   AccEntry* acc_tab;
   uint64_t acc_mask;
@@ -53,6 +62,8 @@ struct Dev {
   uint32_t* exp_cur;  // device word selecting the live expiry buffer
   Globals* g;
   uint64_t acc_max, x_max;  // store capacities (records)
+  HistRow* hist;            // per transfer slot (unsharded engines)
+  uint8_t* hist_side;       // per transfer slot: sides present in hist (0 = no row)
 };
 
 struct Scratch {
@@ -86,6 +97,9 @@ struct Scratch {
   // and the count of resets among the events that ran ok
   uint64_t* pnv;
   uint32_t* pn_src;
+  // history rows of the walker's inserts (k_final copies them to Dev::hist)
+  HistRow* hrow;
+  uint8_t* hside;
   uint64_t* pn_min;
   uint32_t* pn_res;
   void* sort_tmp;

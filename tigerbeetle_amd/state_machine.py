@@ -161,15 +161,19 @@ class StateMachine:
         _lib.check(_lib.lib().tbg_sync(self.h), "sync")
 
     # ---- the rest of the reference surface the replica drives ------------------------------
-    def open(self, accounts, transfers, pending_status):
+    def open(self, accounts, transfers, pending_status, account_balances=None):
         """StateMachine.open (state_machine.zig:527-541): an empty engine takes the forest's objects
-        (records in timestamp order, one TransferPending status per transfer)."""
+        (records in timestamp order, one TransferPending status per transfer, and the
+        account_balances groove's 256 B rows in timestamp order)."""
         acc = np.ascontiguousarray(accounts)
         xf = np.ascontiguousarray(transfers)
         st = np.ascontiguousarray(pending_status, dtype=np.uint8)
+        hb = np.ascontiguousarray(account_balances if account_balances is not None else np.zeros(0, np.uint8),
+                                  dtype=np.uint8)
         _lib.check(_lib.lib().tbg_open(self.h, acc.ctypes.data if len(acc) else None, len(acc),
                                        xf.ctypes.data if len(xf) else None, len(xf),
-                                       st.ctypes.data if len(st) else None), "open")
+                                       st.ctypes.data if len(st) else None,
+                                       hb.ctypes.data if len(hb) else None, len(hb) // 256), "open")
 
     def reset(self):
         """StateMachine.reset (state_machine.zig:486-501)."""
