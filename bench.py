@@ -126,6 +126,10 @@ def parse():
     p.add_argument("--resolver", default="relax", choices=["relax", "wait", "off"],
                    help="balance-limit windows: windowed relaxation (default), wait-based walkers, walker only")
     p.add_argument("--verify", action="store_true", help="setup all ok; cfg1/cfg2: every transfer ok")
+    p.add_argument("--host-fed-transfers", type=int, default=None,
+                   help="cfg1/cfg2: after the timed run, commit this many further transfers of the same stream "
+                        "from pinned host memory (tbg_commit_window_host, H2D overlapped with compute) and report "
+                        "it as `host_fed` (never `value`); default 8 windows, 0 = off")
     p.add_argument("--change-log", action="store_true",
                    help="engine keeps the write-back change log (TBG_FLAG_CHANGE_LOG): its device cost")
     a = p.parse_args()
@@ -138,6 +142,8 @@ def parse():
             setattr(a, k, c[k])
     if a.warmup is None:
         a.warmup = 256 if a.config == "cfg2" else 32
+    if a.host_fed_transfers is None:
+        a.host_fed_transfers = 8 * min(a.window, WINDOW_BATCHES_MAX) * BATCH if a.config in ("cfg1", "cfg2") else 0
     a.tick = c["tick"]
     return a
 
@@ -187,6 +193,54 @@ def host_cpu():
     except (AttributeError, OSError):
         usable = None
     return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+
+
+def host_fed(args, sm, torch, first, n_acc, seed, win):
+    """The replica-shaped input path: `n` further transfers of the same stream staged in pinned host
+    memory, committed with tbg_commit_window_host (each window's H2D on a copy stream overlapping the
+    previous window's kernels, replies copied back to pinned host memory). Timed from the first
+    submission to the last reply."""
+    from tigerbeetle_amd import _lib
+    from tigerbeetle_amd.types import Operation
+
+    L = _lib.lib()
+    n = (args.host_fed_transfers // BATCH) * BATCH
+    d_tmp = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    _lib.check(L.tbg_gen_transfers_uniform(d_tmp.data_ptr(), first, n, seed, n_acc, 0, sm.stream), "gen")
+    sm.sync()
+    h_ev = torch.empty(n * 128, dtype=torch.uint8, pin_memory=True)
+    h_ev.copy_(d_tmp)
+    del d_tmp
+    h_res = torch.zeros(n * 8, dtype=torch.uint8, pin_memory=True)
+    n_win = n // (win * BATCH) + (1 if n % (win * BATCH) else 0)
+    h_base = torch.zeros(n_win * (WINDOW_BATCHES_MAX + 1), dtype=torch.int32, pin_memory=True)
+    torch.cuda.synchronize()
+    ts = sm.prepare_timestamp
+    nb_total = n // BATCH
+    t0 = time.perf_counter()
+    for wi, b0 in enumerate(range(0, nb_total, win)):
+        nb = min(win, nb_total - b0)
+        ns, tss = [], []
+        for _ in range(nb):
+            ts += 1 + BATCH
+            ns.append(BATCH)
+            tss.append(ts)
+        sm.commit_window_host(Operation.create_transfers, h_ev.data_ptr() + b0 * BATCH * 128, ns, tss,
+                              h_res.data_ptr() + b0 * BATCH * 8, h_base.data_ptr() + wi * (WINDOW_BATCHES_MAX + 1) * 4,
+                              True, tss[0])
+    sm.sync()
+    wall = time.perf_counter() - t0
+    sm.prepare_timestamp = ts
+    bases = h_base.numpy().reshape(-1, WINDOW_BATCHES_MAX + 1)
+    fails = 0
+    for wi, b0 in enumerate(range(0, nb_total, win)):
+        fails += int(bases[wi, min(win, nb_total - b0)])
+    return {"value": round(n / wall, 1), "unit": "transfers/s", "transfers": n, "windows": n_win,
+            "window_batches": win, "failed_events": fails, "wall_ms": round(wall * 1000, 3),
+            "h2d_GBs": round(n * 128 / wall / 1e9, 2),
+            "path": "pinned host prepare bodies -> tbg_commit_window_host (two device slots, copy stream "
+                    "overlapping the previous window's kernels) -> replies D2H to pinned host memory"}
 
 
 def cpu_baseline(args, seed):
@@ -487,7 +541,8 @@ def main():
     n_xfer = args.transfers
     seed = args.seed + 1000 * rank  # independent stream per shard
 
-    sm = StateMachine(device=device, batch_max=BATCH, accounts_max=n_acc_total, transfers_max=n_xfer + n_setup,
+    sm = StateMachine(device=device, batch_max=BATCH, accounts_max=n_acc_total,
+                      transfers_max=n_xfer + n_setup + args.host_fed_transfers,
                       window_events_max=win * BATCH,
                       resolver={"relax": True, "wait": "wait", "off": False}[args.resolver],
                       change_log=args.change_log)
@@ -661,6 +716,9 @@ def main():
                         "gpu_ms_timed": round(gpu_ms, 3), "wall_ms_timed": round(wall * 1000, 3)},
             "roofline": roof,
         }
+        if args.host_fed_transfers and cfg in ("cfg1", "cfg2") and world == 1:
+            sm.prepare_timestamp = prepare_ts
+            line["host_fed"] = host_fed(args, sm, torch, n_xfer, n_acc, seed, win)
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, seed)
         print(json.dumps(line), flush=True)

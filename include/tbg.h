@@ -109,6 +109,21 @@ int tbg_commit_window(tbg_engine *engine, uint32_t operation, const void *d_even
                       const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_results,
                       uint32_t *d_batch_base, int auto_pulse, uint64_t prepare_timestamp);
 
+/* Host-fed form of tbg_commit_window: the replica's prepare bodies in host memory
+ * (replica.zig:4151-4158 hands commit the message body). The window is staged into one of two
+ * device slots on a copy stream, so the H2D of the next window overlaps this one's kernels; the
+ * replies come back into h_results / h_batch_base (layout as tbg_commit_window; h_results must hold
+ * one entry per event). Asynchronous: *ticket names the window for tbg_host_window_done. Host
+ * buffers must be pinned (tbg_host_alloc) for the copies to overlap. */
+int tbg_commit_window_host(tbg_engine *engine, uint32_t operation, const void *h_events, uint32_t n_batches,
+                           const uint32_t *batch_events, const uint64_t *batch_timestamps, void *h_results,
+                           uint32_t *h_batch_base, int auto_pulse, uint64_t prepare_timestamp, uint64_t *ticket);
+/* *done = 1 once window `ticket` finished (h_events reusable, replies written). */
+int tbg_host_window_done(tbg_engine *engine, uint64_t ticket, int *done);
+/* Pinned host memory (hipHostMalloc) for message buffers the engine copies from / to. */
+int tbg_host_alloc(size_t bytes, void **out);
+int tbg_host_free(void *p);
+
 /* Waits for all work queued on the engine's stream. TBG_E_WINDOW (reported once) if a window was
  * rejected (see tbg_commit_window). */
 int tbg_sync(tbg_engine *engine);

@@ -19,6 +19,7 @@ EXPORTS = [
     "tbg_shard_prepare_window", "tbg_shard_decide_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
     "tbg_shard_commit_bits_bytes", "tbg_window_changes", "tbg_windows_committed",
     "tbg_open", "tbg_reset", "tbg_prefetch_poll", "tbg_compact", "tbg_checkpoint", "tbg_digest",
+    "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free",
 ]
 
 
@@ -112,6 +113,10 @@ def lib():
         "tbg_compact": ([vp, u64], i32),
         "tbg_checkpoint": ([vp], i32),
         "tbg_digest": ([vp, P(u64)], i32),
+        "tbg_commit_window_host": ([vp, u32, vp, u32, vp, vp, vp, vp, ctypes.c_int, u64, P(u64)], i32),
+        "tbg_host_window_done": ([vp, u64, P(ctypes.c_int)], i32),
+        "tbg_host_alloc": ([ctypes.c_size_t, P(vp)], i32),
+        "tbg_host_free": ([vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -157,6 +157,24 @@ class StateMachine:
                                                 d_batch_base, int(auto_pulse), prepare_timestamp),
                    "commit_window")
 
+    def commit_window_host(self, operation, h_events, batch_events, batch_timestamps, h_results, h_batch_base,
+                           auto_pulse, prepare_timestamp):
+        """Host-fed window (tbg_commit_window_host): pinned host pointers; asynchronous; returns a
+        ticket for window_done()."""
+        nb = len(batch_events)
+        ev = (ctypes.c_uint32 * nb)(*batch_events)
+        ts = (ctypes.c_uint64 * nb)(*batch_timestamps)
+        t = ctypes.c_uint64()
+        _lib.check(_lib.lib().tbg_commit_window_host(self.h, int(operation), h_events, nb, ev, ts, h_results,
+                                                     h_batch_base, int(auto_pulse), prepare_timestamp,
+                                                     ctypes.byref(t)), "commit_window_host")
+        return t.value
+
+    def window_done(self, ticket):
+        done = ctypes.c_int()
+        _lib.check(_lib.lib().tbg_host_window_done(self.h, ticket, ctypes.byref(done)), "host_window_done")
+        return bool(done.value)
+
     def sync(self):
         _lib.check(_lib.lib().tbg_sync(self.h), "sync")
 
