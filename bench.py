@@ -52,16 +52,17 @@ NS_PER_S = 1_000_000_000
 # Algorithmic bytes per event of each kernel (DESIGN.md §5 derives them).
 KERNEL_BYTES_PER_EVENT = {
     # event read 128, two account-table entries 2x32, transfer-id probe 32, window key-map entry 16,
-    # per-event scratch written 72 (code, cls, batch, 4 slots/entries, amt, ...)
-    "prep": 128 + 2 * 32 + 32 + 16 + 72,
-    # event read 128, record append 128, id-table entry 32, two balance pairs read+write 2x64
-    # (atomics), scratch read 40
-    "final": 128 + 128 + 32 + 2 * 64 + 40,
+    # per-event scratch written 72 (code, cls, batch, 4 slots/entries, amt, ...), the stamped record
+    # stored in place 128
+    "prep": 128 + 2 * 32 + 32 + 16 + 72 + 128,
+    # in-place records (every event inserted at its own rank): scratch read 40, two balance adds
+    # 2x64 (memory-side atomics), pending status 1, id read 16 + id-table entry 32
+    "final": 40 + 2 * 64 + 1 + 16 + 32,
 }
 # Windows that extend the sorted transfer prefix (ids strictly increasing above every stored id,
 # DESIGN.md §4): no transfer-id probe (the id is above every stored id), a direct 8 B key-map entry
-# instead of a claim, and no id-table insert in k_final.
-KERNEL_BYTES_PER_EVENT_PREFIX = {"prep": 128 + 2 * 32 + 8 + 72, "final": 128 + 128 + 2 * 64 + 40}
+# instead of a claim, and no id read or id-table insert in k_final.
+KERNEL_BYTES_PER_EVENT_PREFIX = {"prep": 128 + 2 * 32 + 8 + 72 + 128, "final": 40 + 2 * 64 + 1}
 
 CONFIGS = {
     "cfg1": dict(accounts=10_000, transfers=1_000_000, window=32, seed=42, tick=0),
@@ -89,12 +90,15 @@ def warm_phases(sm, nph):
 
 def pmc_traffic(config, kernel, events_per_launch):
     """Per-launch HBM traffic of `kernel` from the committed rocprofv3 PMC summary of this config
-    (profiles/r1/pmc_<config>.json, made by tools/profile.sh + tools/pmc_summary.py: separate
+    (profiles/r<N>/pmc_<config>.json, made by tools/profile.sh + tools/pmc_summary.py: separate
     FETCH_SIZE and WRITE_SIZE passes over the same bench command), scaled to this run's events per
     launch. Returns (raw FETCH+WRITE bytes, bytes with FETCH doubled per the gfx950 streaming-read
     correction, source) or None."""
-    path = os.path.join(ROOT, "profiles", "r1", "pmc_%s.json" % config)
-    if not os.path.exists(path):
+    for rnd in ("r2", "r1"):  # the latest round's summary of this config
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_%s.json" % config)
+        if os.path.exists(path):
+            break
+    else:
         return None
     with open(path) as f:
         k = json.load(f)["kernels"].get(kernel)

@@ -123,6 +123,7 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t windows_applied;  // create_* windows applied (rejected windows excluded), cumulative
   uint32_t final_done;  // k_final blocks finished in a window with pulse_next ops (the last runs k_pn)
   uint32_t pad4;
+  uint64_t win_id_max;  // this window's largest transfer id key (k_ct_prep), folded into x_id_max
 };
 
 // Whether this block is the last of its grid to arrive (every thread of every block calls it once).
@@ -174,6 +175,7 @@ enum : uint32_t {
   C_RANOK = 1u << 20,      // ran ok, then rolled back with its chain (code back-filled linked_event_failed)
   C_HIST = 1u << 21,       // touches an account with flags.history: its history row needs the balances
                            // after it in order, so it runs on the sequential walker
+  C_PREP_REC = 1u << 22,   // k_ct_prep stored the stamped record at slot base + i (k_final keeps it if final)
 };
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

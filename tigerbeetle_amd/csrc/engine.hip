@@ -116,19 +116,26 @@ __device__ inline void mark_hot(Dev d, uint32_t slot, uint32_t epoch) {
 __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
                                                  uint32_t epoch) {
   __shared__ u128 red[256];
+  __shared__ uint4 stage[256 * 4];  // half of each event's record (16 KiB): the in-place record store
   // bit 0 huge amount, bit 1 not claim-free, bit 2 first id above every stored id, bit 3 pulse_next op
   __shared__ uint32_t aux;
+  __shared__ unsigned long long id_max;  // largest id key this block may insert (Globals::x_id_max)
   if (WIN_REJECTED(d.g)) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (threadIdx.x == 0) aux = 0;
+  if (threadIdx.x == 0) {
+    aux = 0;
+    id_max = 0;
+  }
   __syncthreads();
   u128 amount_upper = 0;
+  tb_transfer_t t;  // the event, stamped (also the record a plain create stores in place)
+  bool prec = false;
   if (i < w.E) {
     const uint64_t x_id_max = d.g->x_id_max;
     const uint64_t P = d.g->x_sorted;
     // speculation: claim-free like the previous window (k_claim_fix claims if it was not)
     const bool spec = d.g->mono_prev != 0;
-    tb_transfer_t t = ev[i];
+    t = ev[i];
     const uint8_t* evb = reinterpret_cast<const uint8_t*>(ev);
     const uint32_t b = win_batch(w, i);
     {
@@ -256,6 +263,12 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
               } else {
                 code = TB_CT_OK;
                 cls |= C_INSERT;
+                if (!(f & TB_TRANSFER_PENDING)) {
+                  // the stamped record goes to its own position (stored below): final if every
+                  // earlier event of the window inserts (k_final then neither re-reads the event
+                  // nor stores it)
+                  cls |= C_PREP_REC;
+                }
                 if ((f & TB_TRANSFER_PENDING) && t.timeout > 0) {
                   // if it runs ok, pulse_next = min(pulse_next, expires_at) (:1576-1581)
                   pnv = t.timestamp + (uint64_t)t.timeout * TB_NS_PER_S;
@@ -273,6 +286,8 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
       atomicOr(&aux, 8u);
     }
     if (cls & C_HIST) atomicOr(&aux, 32u);
+    if (cls & C_REACH) atomicMax(&id_max, (unsigned long long)x_id_key(t.id));
+    prec = (cls & C_PREP_REC) != 0;
     // Hot marks: the first marker of an account this window gives it the next dense rank.
     if (cls & C_READS_DR) mark_hot(d, dr_slot, epoch);
     if (cls & C_READS_CR) mark_hot(d, cr_slot, epoch);
@@ -289,6 +304,29 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     if (cls & C_POSTVOID) s.pamt[i] = pamt;  // read only for post/void events (k_final)
     s.ins[i] = 0;
   }
+  // The wave's records at slots base + i0 .. base + i0 + 63, through LDS in two halves (64 B of
+  // each record per round), so each store instruction writes whole 64 B sectors instead of 16 B
+  // pieces of 64 records. Lanes without a record write garbage rows: such a slot is either beyond
+  // the window's insert count or rewritten by k_final (the event ranked there is not in place).
+  if (__ballot(prec) != 0) {
+    const uint32_t lane = threadIdx.x & 63, i0 = i - lane;
+    const uint32_t nrec = i0 < w.E ? min(64u, w.E - i0) : 0u;
+    uint4* ws = stage + (threadIdx.x >> 6) * 256;
+    const uint4* src = reinterpret_cast<const uint4*>(&t);
+    uint4* dst = reinterpret_cast<uint4*>(d.xr + (d.g->x_count + i0));
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      wave_sync();
+#pragma unroll
+      for (int q = 0; q < 4; q++) ws[lane * 4 + q] = src[half * 4 + q];
+      wave_sync();
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t idx = k * 64 + lane, r = idx >> 2, q = idx & 3;
+        if (r < nrec) st_stream(dst + r * 8 + half * 4 + q, ws[idx]);
+      }
+    }
+  }
   // Window amount bound: block reduction into this block's partial (k_prep_reduce sums them; a
   // same-address atomic per block serializes thousands of blocks on one memory-side word).
   red[threadIdx.x] = ((uint64_t)(amount_upper >> 64) != 0) ? 0 : amount_upper;
@@ -300,6 +338,8 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   if (threadIdx.x == 0) {
     s.blk_amt[blockIdx.x] = red[0];
     s.blk_aux[blockIdx.x] = aux;
+    // an upper bound of every id this window may store (the failures' ids included)
+    if (id_max) atomicMax(reinterpret_cast<unsigned long long*>(&d.g->win_id_max), id_max);
   }
 }
 
@@ -344,6 +384,8 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
     // component walkers, which run before k_walk, read it from here)
     const u128 sum = g->ovf_bound + g->batch_amount_sum;
     g->small_win = !g->batch_huge && sum >= g->ovf_bound && (uint64_t)(sum >> 64) == 0;
+    if (g->win_id_max > g->x_id_max) g->x_id_max = g->win_id_max;
+    g->win_id_max = 0;
   }
 }
 
@@ -890,12 +932,6 @@ __device__ inline void rw_post_void(uint4* r, const tb_transfer_t* pending, u128
   r[7].y = (p7.y & 0xFFFFu) | (r[7].y & 0xFFFF0000u);
 }
 
-// Wave-scope LDS ordering: this wave's LDS writes are visible to all of its lanes after the call.
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Final write-out, one event per thread. The 128 B event records pass through LDS (8 KiB per wave):
 // each wave loads its 64 input records with contiguous 16 B-per-lane loads, and stores its inserted
@@ -907,22 +943,12 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   __shared__ unsigned long long ldsm[SEG / 64];
   __shared__ uint4 stage[SEG * 8];  // one 128 B record per event: 128 KiB
   if (WIN_REJECTED(d.g)) return;
-  unsigned long long id_key = 0;  // this thread's inserted transfer id, for Globals::x_id_max
   const bool prefix_win = XFER && (d.g->win_flags & 2u) != 0;  // k_prep_reduce
   const uint32_t E = w.E;
   const uint32_t i = blockIdx.x * SEG + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t i0 = i - lane;  // the wave's first event
   uint4* ws = stage + (threadIdx.x >> 6) * 512;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(ev_bytes) + (size_t)i0 * 8;
-    const uint32_t nrec = i0 < E ? min(64u, E - i0) : 0u;
-#pragma unroll
-    for (uint32_t q = 0; q < 8; q++) {
-      const uint32_t k = q * 64 + lane;
-      if ((k >> 3) < nrec) ws[k] = ld_stream(src + k);
-    }
-  }
   uint32_t cls = 0, code = TB_CT_OK;
   bool ins = false;
   if (i < E) {
@@ -937,6 +963,24 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
   const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
   const uint64_t xbase = d.g->base;
+  // k_ct_prep already stored the stamped input record of each plain create it expected to insert
+  // at its own position (base + i). That record is final when the event inserts at rank i (no
+  // earlier event of the window failed) and is neither W (walker record) nor a post/void (posting
+  // record) nor pending (status and expiry below need its fields). A wave whose lanes are all such
+  // events (or insert nothing) neither loads its input rows nor stores records.
+  const bool direct = XFER && ins && rins == i && !(cls & (C_W | C_POSTVOID | C_PENDING)) && (cls & C_PREP_REC);
+  const bool wave_rec = __ballot(ins && !direct) != 0;
+  // a wave that stores records stores all of its inserted ones (one contiguous run)
+  const bool in_place = direct && !wave_rec;
+  if (wave_rec) {
+    const uint4* src = reinterpret_cast<const uint4*>(ev_bytes) + (size_t)i0 * 8;
+    const uint32_t nrec = i0 < E ? min(64u, E - i0) : 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+      const uint32_t k = q * 64 + lane;
+      if ((k >> 3) < nrec) ws[k] = ld_stream(src + k);
+    }
+  }
   wave_sync();
   // this event's output record (the input record, stamped; W events carry theirs in s.t2)
   uint4 rec[8];
@@ -944,15 +988,12 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     const uint4* t2 = reinterpret_cast<const uint4*>(&s.t2[i]);
 #pragma unroll
     for (int q = 0; q < 8; q++) rec[q] = t2[q];
-  } else {
+  } else if (wave_rec) {
 #pragma unroll
     for (int q = 0; q < 8; q++) rec[q] = ws[lane * 8 + q];
-  }
-  if (XFER && ins) id_key = x_id_key(rw_u128(rec[0]));
-  if (XFER) {
-    const unsigned long long m = block_max_u64<SEG / 64>(id_key, ldsm);
-    // a no-return atomic: the wave does not wait for it (unlike k_ct_prep's returning amount add)
-    if (threadIdx.x == 0 && m > d.g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&d.g->x_id_max), m);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; q++) rec[q] = make_uint4(0, 0, 0, 0);
   }
   if (i < E) {
     const uint32_t b = s.batch[i];
@@ -1001,7 +1042,15 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
           a_cr.issue(&cra->credits_posted, a, small);
         }
       }
-      if (ins) {
+      if (ins && in_place) {
+        // the record is in place (k_ct_prep): index it unless the window extends the sorted prefix
+        const uint64_t slot = xbase + rins;
+        if (!prefix_win) {
+          const tb_uint128_t id = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].id;
+          x_insert(d.x_tab, d.x_mask, id, (uint32_t)slot);
+        }
+        d.xstatus[slot] = 0;
+      } else if (ins) {
         const uint64_t slot = xbase + rins;
         if (!wev) {
           rw_stamp(rec, win_ts(w, b, i));
@@ -1048,11 +1097,12 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
         atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->limited_accounts), 1ull);
     }
   }
-  // Compact this wave's inserted records in LDS, then store them as one contiguous run.
+  // Compact this wave's inserted records in LDS, then store them as one contiguous run (a wave
+  // with only in-place records stores nothing).
   const uint32_t r0 = __shfl(rins, 0);
-  const uint32_t nins = (uint32_t)__popcll(__ballot(ins));
+  const uint32_t nins = wave_rec ? (uint32_t)__popcll(__ballot(ins)) : 0u;
   wave_sync();
-  if (ins) {
+  if (ins && wave_rec) {
 #pragma unroll
     for (int q = 0; q < 8; q++) ws[(rins - r0) * 8 + q] = rec[q];
   }

@@ -106,6 +106,13 @@ struct Scratch {
   size_t sort_tmp_bytes;
 };
 
+// Wave-scope LDS ordering: this wave's LDS writes are visible to all of its lanes after the call.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ------------------------------------------------------------------------------------------------
 // Scan helpers (wave64 shuffles + one LDS word per wave).
 // ------------------------------------------------------------------------------------------------
