@@ -7,7 +7,8 @@ src/tigerbeetle/benchmark_load.zig:206-327). `--config` selects the other BASELI
   cfg3  Zipf(1.2) hot accounts, debits_must_not_exceed_credits on >= 50 % (incl. the top 1000),
         pre-funded from treasury accounts (funding untimed), 10M transfers
   cfg4  two-phase (30 % pending, post/void, expiry) + linked chains with injected failures,
-        synthetic clock +1 s per batch (a pulse is due before every batch), 10M transfers
+        synthetic clock +1 s per batch (a pulse is due before every batch), 10M transfers, in
+        128-batch windows whose inner pulses the engine models (csrc/xwin.h)
   cfg5  hash-sharded over the N GPUs (default when N > 1): 12.5M accounts and 125M uniform transfers
         per GPU (100M / 1B at N = 8), ~(N-1)/N of the transfers cross-shard; one stream for the whole
         job, resident in every GPU's HBM; per window two RCCL all-reduces: the per-event owner facts
@@ -68,7 +69,7 @@ CONFIGS = {
     "cfg1": dict(accounts=10_000, transfers=1_000_000, window=32, seed=42, tick=0),
     "cfg2": dict(accounts=1_000_000, transfers=100_000_000, window=128, seed=44, tick=0),
     "cfg3": dict(accounts=1_000_000, transfers=10_000_000, window=32, seed=45, tick=0),
-    "cfg4": dict(accounts=1_000_000, transfers=10_000_000, window=1, seed=46, tick=NS_PER_S),
+    "cfg4": dict(accounts=1_000_000, transfers=10_000_000, window=128, seed=46, tick=NS_PER_S),
     # per GPU (weak scaling): 100M accounts / 1B transfers at 8 GPUs
     "cfg5": dict(accounts=12_500_000, transfers=125_000_000, window=64, seed=47, tick=0),
 }

@@ -46,6 +46,9 @@ typedef struct tbg_config {
 /* Resolve balance-limit windows with the wait-based account walkers (resolver.h) instead of the
    default windowed relaxation (relax.h). Same results; kept for comparison. */
 #define TBG_FLAG_RES_WAIT 4u
+/* Reject (TBG_E_WINDOW) every multi-batch window in which a pulse falls due, instead of modelling
+   the pulses inside windows that span a second or more (tigerbeetle_amd/csrc/xwin.h). */
+#define TBG_FLAG_NO_XWIN 16u
 
 #define TBG_OK 0
 #define TBG_E_INVALID (-1)   /* input_valid() would reject the request */
@@ -53,8 +56,9 @@ typedef struct tbg_config {
 #define TBG_E_DEVICE (-3)    /* HIP runtime / device failure: fatal */
 #define TBG_E_STATE (-4)     /* API misuse (e.g. commit timestamp not increasing) */
 #define TBG_E_UNSUPPORTED (-5) /* sharded engine: a window outside the sharded class (nothing applied) */
-#define TBG_E_WINDOW (-6)    /* a commit window spanned a due pulse: it and every window queued after it
-                                were skipped whole (pulse included); resubmit them in smaller windows */
+#define TBG_E_WINDOW (-6)    /* a commit window spanned a due pulse it could not model: it and every window
+                                queued after it were skipped (see tbg_commit_window); resubmit them in
+                                smaller windows */
 
 /* StateMachine.init (state_machine.zig:455-477) / deinit (:479-484). */
 int tbg_create(const tbg_config *config, tbg_engine **out);
@@ -100,11 +104,14 @@ int tbg_commit_device(tbg_engine *engine, uint32_t operation, uint64_t timestamp
  * per batch: batch b's replies are entries [d_batch_base[b], d_batch_base[b+1]), each with a
  * batch-relative index. With `auto_pulse`, the pulse decision for the first batch
  * (pulse_next <= prepare_timestamp) and the pulse run first, on the device. A pulse that expires
- * nothing inside the window (after a post/void reset pulse_next) is modelled exactly; a window in
- * which a pulse with expiries would fall due is rejected whole on the device (nothing applied, its
- * pulse included, and every window queued after it skipped too): tbg_sync() returns TBG_E_WINDOW
- * and tbg_windows_committed() tells how many windows were applied. Asynchronous on the engine
- * stream. n_batches <= 128, total events <= window_events_max. */
+ * nothing inside the window (after a post/void reset pulse_next) is modelled exactly. A window whose
+ * batches span a second or more models the pulses with expiries inside it too (csrc/xwin.h) when no
+ * decision of it reads a balance, it writes no history row and no inner pulse can reach the scan
+ * cap; otherwise it is rejected after its first pulse (that pulse applied, nothing else). Any other
+ * window in which a pulse with expiries would fall due is rejected whole (its pulse included). A
+ * rejected window skips every window queued after it too: tbg_sync() returns TBG_E_WINDOW and
+ * tbg_windows_committed() tells how many windows were applied; resubmitting the same batches is
+ * exact. Asynchronous on the engine stream. n_batches <= 128, total events <= window_events_max. */
 int tbg_commit_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_batches,
                       const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_results,
                       uint32_t *d_batch_base, int auto_pulse, uint64_t prepare_timestamp);

@@ -7,6 +7,7 @@ dumps).
 - cfg2: uniform transfers, device-generated exactly as bench.py generates them;
 - cfg4 mixed at window scale: two-phase, posts/voids, chains with injected failures in 1M-event
   windows (no tick inside a window: the component walkers and the pulse_next replay at scale);
+- cfg4 as bench.py runs it: +1 s per batch, 128-batch windows with ~127 pulses inside each;
 - cfg3: Zipf(1.2) with limits, pre-funded, bench.py's 32-batch windows (the account-parallel
   resolver at 262K-event windows);
 - cfg5: G = 8 hash shards on one GPU at 128-batch windows, 12.5M accounts' shape scaled to 1M.
@@ -107,6 +108,40 @@ def test_geometry_cfg4_mixed_windows():
             assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
         st = gpu.stats()
         assert st["component_events"] + st["walker_events"] > 0  # the order-dependent part ran
+        _check_digest(gpu, ref)
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_geometry_cfg4_bench_windows_with_pulses():
+    """bench.py's cfg4 exactly: +1 s per batch in 128-batch windows on 1M accounts, so ~127 pulses
+    with expiries fall due inside every window (csrc/xwin.h); replies, pulse_next_timestamp after
+    every window, the stores and the digest vs the restatement run batch by batch."""
+    from test_gpu_xwin import commit_ticked, oracle_ticked
+    from tigerbeetle_amd import StateMachine
+    from tigerbeetle_amd.types import NS_PER_S
+
+    n_win, seed = 3, 46
+    n_x = n_win * 128 * BM
+    gpu = StateMachine(batch_max=BM, accounts_max=N_ACC, transfers_max=n_x, window_events_max=128 * BM)
+    ref = OracleStateMachine(batch_max=BM)
+    try:
+        _accounts(gpu, ref, seed)
+        host = workload.transfers_cfg4(0, n_x, seed, N_ACC, BM)
+        inner = 0
+        for w in range(n_win):
+            xb = _batches(host, w * 128 * BM, 128 * BM)
+            g, rej = commit_ticked(gpu, Operation.create_transfers, xb, [NS_PER_S] * 128)
+            r, n_inner = oracle_ticked(ref, Operation.create_transfers, xb, [NS_PER_S] * 128)
+            assert not rej, f"window {w} rejected"
+            bad = [b for b in range(128) if g[b] != r[b]]
+            assert not bad, f"window {w}: batches {bad[:8]} differ"
+            assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
+            inner += n_inner
+        assert inner > n_win * 100
         _check_digest(gpu, ref)
         _compare_final(gpu, ref)
     finally:

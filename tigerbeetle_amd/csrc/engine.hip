@@ -203,7 +203,12 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
                 cls |= C_HIST;
             }
             if (code == CONT && id_tslot != NONE32) code = pv_exists(t, d.xr[id_tslot], p);
-            if (code == CONT) code = pv_status(d.xstatus[p_tslot]);
+            if (code == CONT) {
+              uint8_t pst = d.xstatus[p_tslot];
+              // a pulse of the window expired p at or before this batch (xwin.h)
+              if (pst == TB_PENDING_PENDING && xw_expired_before(w, p, b)) pst = TB_PENDING_EXPIRED;
+              code = pv_status(pst);
+            }
             if (code == CONT) {
               cls |= C_INSERT;
               pamt = U(p.amount);
@@ -273,6 +278,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
                   // if it runs ok, pulse_next = min(pulse_next, expires_at) (:1576-1581)
                   pnv = t.timestamp + (uint64_t)t.timeout * TB_NS_PER_S;
                   cls |= C_PNOP;
+                  if (w.xwin) s.pn_rb[i] = 0xFFFFu;  // not removed (k_xwin_rb)
                 }
               }
             }
@@ -853,6 +859,8 @@ __device__ void pn_replay(const Dev& d, const Scratch& s, const WinDesc& w, unsi
   if (threadIdx.x == 0) d.g->pulse_next = pn;
 }
 
+#include "xwin.h"
+
 // ------------------------------------------------------------------------------------------------
 // final: ordered replies + insert ranks + effects (one event per thread, one segment per block)
 // ------------------------------------------------------------------------------------------------
@@ -1138,7 +1146,8 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     gw->light_count = 0;
     gw->cpw_done = 0;
   }
-  const uint32_t wf = XFER ? d.g->win_flags : 0u;
+  // (windows with pulses inside replay pulse_next in k_xwin_replay)
+  const uint32_t wf = (XFER && !w.xwin) ? d.g->win_flags : 0u;
   if (wf & 8u) {
     // a post/void may reset pulse_next: this segment's summary, then the last block to finish
     // replays the window's ops in event order into pulse_next
@@ -1167,9 +1176,11 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
 // reset only lowers it); entries the window creates expire >= its first timestamp + 1 s.
 struct WinChk {
   uint32_t nb;
+  uint32_t xwin;  // the window models the pulses inside it (xwin.h)
   uint64_t T_last, first_ts;
 };
 __device__ inline bool window_spans_pulse(const WinChk& c, uint64_t pulse_next) {
+  if (c.xwin) return false;
   return c.nb > 1 && (c.T_last >= pulse_next || c.T_last >= c.first_ts + TB_NS_PER_S);
 }
 
@@ -1266,7 +1277,8 @@ __global__ void __launch_bounds__(1024) k_pulse(Dev d, Scratch s, uint64_t T, ui
   const uint64_t pn_after = select_all ? (n_alt > 0 ? g->next_min : TB_TIMESTAMP_MAX) : prefix_hi;
   const uint64_t thr_e = prefix_hi;
   const uint32_t thr_s = prefix_lo;
-  if (window_spans_pulse(chk, pn_after)) {
+  // (a window modelling its pulses needs this one to have finished its scan)
+  if (window_spans_pulse(chk, pn_after) || (chk.xwin && !select_all)) {
     __syncthreads();
     if (threadIdx.x == 0) {
       atomicOr(&g->window_error, 1u);

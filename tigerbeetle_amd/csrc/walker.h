@@ -6,6 +6,19 @@
 #include "sm_logic.h"
 #include "window.h"
 
+// An entry the expires_at scan can return (composite key range, lsm/composite_key.zig:25-57).
+__device__ inline bool xw_visible(uint64_t timestamp, uint64_t expires_at) {
+  return !(timestamp >> 63) && expires_at <= TB_TIMESTAMP_MAX;
+}
+
+// In a window with pulses inside (xwin.h): whether a post/void at batch b finds pending transfer p
+// already expired by one of the window's pulses (the first batch with T >= its expires_at).
+__device__ inline bool xw_expired_before(const WinDesc& w, const tb_transfer_t& p, uint32_t b) {
+  if (!w.xwin || p.timeout == 0) return false;
+  const uint64_t exp = expires_at_of(p);
+  return xw_visible(p.timestamp, exp) && exp <= w.T[b];
+}
+
 // Window key map (see BEntry). `epoch` is the window number.
 __device__ inline tb_uint128_t bkey(const uint8_t* ev, uint32_t owner, uint32_t is_pid) {
   return *reinterpret_cast<const tb_uint128_t*>(ev + (size_t)owner * 128 + (is_pid ? 64 : 0));
@@ -234,7 +247,9 @@ struct Walker {
     if (s.id_tslot[i] != NONE32) return pv_exists(t, d.xr[s.id_tslot[i]], p);
     const int32_t c = bmap_committed(s.bmap, s.id_ent[i], epoch);
     if (c >= 0) return pv_exists(t, s.t2[c], p);
-    r = pv_status(pc >= 0 ? s.bstatus[pc] : d.xstatus[pslot]);
+    uint8_t pst = pc >= 0 ? s.bstatus[pc] : d.xstatus[pslot];
+    if (pst == TB_PENDING_PENDING && xw_expired_before(*w, p, s.batch[i])) pst = TB_PENDING_EXPIRED;
+    r = pv_status(pst);
     if (r != CONT) return r;
     commit_record(i, pv_record(t, p, amount));
     if (p.timeout > 0 && expires_at_of(p) <= t.timestamp) return TB_CT_PENDING_TRANSFER_EXPIRED;

@@ -13,8 +13,20 @@ struct WinDesc {
   uint32_t nb;             // batches in the window
   uint32_t E;              // events in the window
   uint32_t off[MAXB + 1];  // event offset of each batch; off[nb] = E
+  uint32_t xwin;           // pulses inside the window are modelled (xwin.h): it spans >= 1 s
   uint64_t T[MAXB];        // commit timestamp of each batch
 };
+
+// The first batch of the window whose pulse check (T_b >= expires_at) finds an entry due: the pulse
+// that expires it (xwin.h; MAXB = window's nb when none).
+__device__ inline uint32_t xw_due(const WinDesc& w, uint64_t expires_at) {
+  uint32_t lo = 0, hi = w.nb;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (w.T[mid] >= expires_at) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
 
 __device__ inline uint32_t win_batch(const WinDesc& w, uint32_t i) {
   uint32_t lo = 0, hi = w.nb - 1;
@@ -100,6 +112,14 @@ struct Scratch {
   // history rows of the walker's inserts (k_final copies them to Dev::hist)
   HistRow* hrow;
   uint8_t* hside;
+  // windows with pulses inside (xwin.h): per in-window pending creation, the batch of the committed
+  // post/void that removed it; per batch: due counts, minimum live expires_at after its pulse
+  // (segment tree over MAXB leaves), minimum creation expiry and reset candidate
+  uint16_t* pn_rb;
+  uint32_t* xw_cnt;             // [MAXB]
+  unsigned long long* xw_tree;  // [2 * MAXB]
+  unsigned long long* xw_minx;  // [MAXB]
+  unsigned long long* xw_miny;  // [MAXB]
   uint64_t* pn_min;
   uint32_t* pn_res;
   void* sort_tmp;
