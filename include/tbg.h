@@ -194,6 +194,16 @@ int tbg_checkpoint(tbg_engine *engine);
  * them), out[3] pulse_next_timestamp. Synchronizes. */
 int tbg_digest(tbg_engine *engine, uint64_t out[4]);
 
+/* TigerBeetle's checksum (vsr/checksum.zig:50-59: AEGIS-128L MAC, zero key) of n messages in HBM:
+ * message k is the d_sizes[k] bytes at d_base + d_offsets[k]; its u128 checksum (little-endian, as
+ * the Header fields store it) lands at d_out + 16 k. The replacement for checksum() on the prepare
+ * bodies and headers a replica verifies (Header.valid_checksum / valid_checksum_body,
+ * vsr/message_header.zig:105-137) and the replies it signs (replica.zig:4199-4202), for whole commit
+ * windows or AOF files at once (tigerbeetle_amd/csrc/checksum.hip). Any alignment; 16-byte-aligned
+ * messages load fastest. Asynchronous on `stream` (a hipStream_t; NULL = the default stream). */
+int tbg_checksum(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_sizes, uint32_t n, void *d_out,
+                 void *stream);
+
 /* Test hook mirroring the harness `setup` action (state_machine.zig:2545-2561). */
 int tbg_setup_balances(tbg_engine *engine, const tb_uint128_t *id, const tb_uint128_t *debits_pending,
                        const tb_uint128_t *debits_posted, const tb_uint128_t *credits_pending,

@@ -19,7 +19,7 @@ EXPORTS = [
     "tbg_shard_prepare_window", "tbg_shard_decide_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
     "tbg_shard_commit_bits_bytes", "tbg_window_changes", "tbg_windows_committed",
     "tbg_open", "tbg_reset", "tbg_prefetch_poll", "tbg_compact", "tbg_checkpoint", "tbg_digest",
-    "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free",
+    "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free", "tbg_checksum",
 ]
 
 
@@ -42,6 +42,7 @@ FLAG_NO_RESOLVER = 1
 FLAG_NO_COMPONENTS = 2
 FLAG_RES_WAIT = 4
 FLAG_CHANGE_LOG = 8
+FLAG_NO_XWIN = 16
 
 
 class Stats(ctypes.Structure):
@@ -117,6 +118,7 @@ def lib():
         "tbg_host_window_done": ([vp, u64, P(ctypes.c_int)], i32),
         "tbg_host_alloc": ([ctypes.c_size_t, P(vp)], i32),
         "tbg_host_free": ([vp], i32),
+        "tbg_checksum": ([vp, vp, vp, u32, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

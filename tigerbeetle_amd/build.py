@@ -5,7 +5,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = ["csrc/engine.hip", "csrc/workload.hip"]
+SOURCES = ["csrc/engine.hip", "csrc/workload.hip", "csrc/checksum.hip"]
 HEADERS = sorted("csrc/" + f for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith((".h", ".inc"))) + [
     "../include/tb_types.h", "../include/tbg.h"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared", "-Wall"]
