@@ -204,6 +204,59 @@ int tbg_digest(tbg_engine *engine, uint64_t out[4]);
 int tbg_checksum(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_sizes, uint32_t n, void *d_out,
                  void *stream);
 
+/* tbg_commit_window's `auto_pulse` = TBG_WINDOW_LOG: the batches come from a replica's log (an AOF,
+ * the journal), where every pulse is a prepare of its own (vsr.Operation.pulse, replica.zig:
+ * 9459-9487) committed with tbg_commit(TB_OP_PULSE): no pulse is run or modelled between or before
+ * the window's batches. */
+#define TBG_WINDOW_LOG 2
+
+/* Client-side reply demultiplexing (DemuxerType, state_machine.zig:133-176): a client that packed
+ * several requests' events into one create_* batch splits the reply per request. init takes the
+ * reply body (its results are rewritten in place); each decode(event_offset, event_count) returns
+ * the results of the next request, indexes rebased to it, with monotonically increasing disjoint
+ * ranges. Lookups and queries are not batched: event_offset must be 0 and the whole reply is
+ * returned. TBG_E_INVALID for other operations or misaligned replies. Host-only. */
+typedef struct tbg_demuxer {
+    void *results;
+    uint32_t count;
+    uint32_t operation;
+} tbg_demuxer;
+int tbg_demux_init(tbg_demuxer *demuxer, uint32_t operation, void *reply, uint32_t reply_size);
+int tbg_demux_decode(tbg_demuxer *demuxer, uint32_t event_offset, uint32_t event_count, void **results,
+                     uint32_t *results_size);
+
+/* Replay of an append-only file of prepares (aof.zig:23-55: entries of magic u128, 4080 B of
+ * metadata, then the prepare message, each padded to 4096 B) into the engine, as a replica applies
+ * its log: entries are checked in file order like AOF.Iterator.next (aof.zig:176-228: short read,
+ * magic, header checksum, body checksum, hash chain parent == previous checksum) — every checksum of
+ * the file verified on the GPU in bulk (tbg_checksum) — and the valid prefix is applied: runs of
+ * create_accounts / create_transfers prepares as commit windows (TBG_WINDOW_LOG, batch timestamps
+ * = header.timestamp), vsr pulse prepares as pulses; control-plane prepares, lookups and queries are
+ * skipped (they change no state). Returns TBG_OK for a clean file, TBG_E_INVALID with
+ * stats.error / stats.error_entry at the first bad entry (everything before it applied). `h_aof` is
+ * host memory (e.g. an mmap of the file). */
+#define TBG_AOF_OK 0
+#define TBG_AOF_SHORT_READ 1      /* error.AOFShortRead */
+#define TBG_AOF_MAGIC 2           /* error.AOFMagicNumberMismatch */
+#define TBG_AOF_CHECKSUM 3        /* error.AOFChecksumMismatch */
+#define TBG_AOF_BODY_CHECKSUM 4   /* error.AOFBodyChecksumMismatch */
+#define TBG_AOF_CHAIN 5           /* error.AOFChecksumChainMismatch */
+#define TBG_AOF_INPUT 6           /* a create_* prepare body that input_valid() rejects */
+#define TBG_AOF_NO_CHAIN 1u       /* flags: skip the hash-chain check (Iterator.validate_chain = false) */
+typedef struct tbg_aof_stats {
+    uint64_t entries;        /* entries applied (prepares, pulses and skipped ones) */
+    uint64_t prepares;       /* create_* prepares committed */
+    uint64_t pulses;         /* pulse prepares committed */
+    uint64_t skipped;        /* other prepares */
+    uint64_t windows;        /* commit windows launched */
+    uint64_t events;         /* create_* events committed */
+    uint64_t failed_events;  /* of which failed with a result code */
+    int64_t error_entry;     /* index of the first bad entry, -1 if none */
+    int32_t error;           /* TBG_AOF_* */
+    int32_t reserved;
+} tbg_aof_stats;
+int tbg_aof_replay(tbg_engine *engine, const void *h_aof, uint64_t size, uint32_t flags, tbg_aof_stats *stats);
+
 /* Test hook mirroring the harness `setup` action (state_machine.zig:2545-2561). */
 int tbg_setup_balances(tbg_engine *engine, const tb_uint128_t *id, const tb_uint128_t *debits_pending,
                        const tb_uint128_t *debits_posted, const tb_uint128_t *credits_pending,

@@ -20,6 +20,7 @@ EXPORTS = [
     "tbg_shard_commit_bits_bytes", "tbg_window_changes", "tbg_windows_committed",
     "tbg_open", "tbg_reset", "tbg_prefetch_poll", "tbg_compact", "tbg_checkpoint", "tbg_digest",
     "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free", "tbg_checksum",
+    "tbg_demux_init", "tbg_demux_decode", "tbg_aof_replay",
 ]
 
 
@@ -52,6 +53,22 @@ class Stats(ctypes.Structure):
                 ("resolver_events", ctypes.c_uint64), ("component_events", ctypes.c_uint64),
                 ("sorted_transfers", ctypes.c_uint64)]
 
+
+class Demuxer(ctypes.Structure):
+    _fields_ = [("results", ctypes.c_void_p), ("count", ctypes.c_uint32), ("operation", ctypes.c_uint32)]
+
+
+class AofStats(ctypes.Structure):
+    _fields_ = [("entries", ctypes.c_uint64), ("prepares", ctypes.c_uint64), ("pulses", ctypes.c_uint64),
+                ("skipped", ctypes.c_uint64), ("windows", ctypes.c_uint64), ("events", ctypes.c_uint64),
+                ("failed_events", ctypes.c_uint64), ("error_entry", ctypes.c_int64), ("error", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+AOF_ERRORS = {0: None, 1: "AOFShortRead", 2: "AOFMagicNumberMismatch", 3: "AOFChecksumMismatch",
+              4: "AOFBodyChecksumMismatch", 5: "AOFChecksumChainMismatch", 6: "InvalidPrepareBody"}
+AOF_NO_CHAIN = 1
+WINDOW_LOG = 2
 
 _lib = None
 
@@ -119,6 +136,9 @@ def lib():
         "tbg_host_alloc": ([ctypes.c_size_t, P(vp)], i32),
         "tbg_host_free": ([vp], i32),
         "tbg_checksum": ([vp, vp, vp, u32, vp, vp], i32),
+        "tbg_demux_init": ([P(Demuxer), u32, vp, u32], i32),
+        "tbg_demux_decode": ([P(Demuxer), u32, u32, P(vp), P(u32)], i32),
+        "tbg_aof_replay": ([vp, vp, u64, u32, P(AofStats)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -653,11 +653,14 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
     }
     return;
   }
-  if (threadIdx.x == 0 && d.g->cpw_done) {  // cpw.h walked W; fold below
-    d.g->cpw_events_total += w_count;
-    d.g->events_total += w.E;
+  if (d.g->cpw_done) {  // cpw.h walked W; k_wfold folds the outcomes with the whole grid
+    if (threadIdx.x == 0) {
+      d.g->cpw_events_total += w_count;
+      d.g->events_total += w.E;
+    }
+    return;
   }
-  if (threadIdx.x == 0 && !d.g->cpw_done) {
+  if (threadIdx.x == 0) {
     Walker wk;
     wk.d = d;
     wk.s = s;
@@ -684,6 +687,27 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
   for (uint32_t j = threadIdx.x; j < nseg; j += WALK_THREADS) {
     if (sbad[j]) s.cnt_bad[j] += sbad[j];
     if (sins[j]) s.cnt_ins[j] += sins[j];
+  }
+}
+
+// The W outcomes of a component-walked window into the segment counts (k_walk folds the sequential
+// walker's own): per block an LDS histogram over the segments, then one global add per non-zero bin.
+__global__ void __launch_bounds__(1024) k_wfold(Dev d, Scratch s, uint32_t nseg) {
+  __shared__ uint32_t sbad[MAX_SEGS], sins[MAX_SEGS];
+  if (WIN_REJECTED(d.g) || !d.g->cpw_done) return;
+  const uint32_t w_count = d.g->w_count;
+  for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) sbad[j] = sins[j] = 0;
+  __syncthreads();
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < w_count; k += gridDim.x * blockDim.x) {
+    const uint32_t i = s.wlist[k];
+    const uint32_t seg = i / SEG;
+    if (s.code[i] != TB_CT_OK) atomicAdd(&sbad[seg], 1u);
+    if (s.ins[i]) atomicAdd(&sins[seg], 1u);
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) {
+    if (sbad[j]) atomicAdd(&s.cnt_bad[j], sbad[j]);
+    if (sins[j]) atomicAdd(&s.cnt_ins[j], sins[j]);
   }
 }
 
@@ -845,6 +869,11 @@ __device__ void pn_replay(const Dev& d, const Scratch& s, const WinDesc& w, unsi
     __syncthreads();
     if (op == 2 && before == v) atomicMin(&first_eff, k);
     __syncthreads();
+    if (first_eff != NONE32 && w.log) {
+      // a log's window: no pulse until the log's next pulse prepare, so timestamp_min stands
+      pn = TB_TIMESTAMP_MIN;
+      break;
+    }
     if (first_eff != NONE32) {
       // reset to timestamp_min (:1706-1707); the next batch's pulse finds nothing due
       i = w.off[b + 1];
@@ -1385,3 +1414,4 @@ __global__ void k_setup(Dev d, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dp
 }
 
 #include "host.inc"
+#include "aof.inc"

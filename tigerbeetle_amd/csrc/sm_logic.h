@@ -7,7 +7,7 @@
 #include "dev_common.h"
 
 // create_transfer head (state_machine.zig:1465-1468).
-__device__ inline uint32_t ct_head(const tb_transfer_t& t) {
+__device__ __attribute__((always_inline)) inline uint32_t ct_head(const tb_transfer_t& t) {
   if (t.flags & TB_TRANSFER_PADDING_MASK) return TB_CT_RESERVED_FLAG;
   const u128 id = U(t.id);
   if (id == 0) return TB_CT_ID_MUST_NOT_BE_ZERO;
@@ -16,7 +16,7 @@ __device__ inline uint32_t ct_head(const tb_transfer_t& t) {
 }
 
 // create_transfer field validation, single-phase/pending branch (:1474-1489).
-__device__ inline uint32_t ct_validate(const tb_transfer_t& t) {
+__device__ __attribute__((always_inline)) inline uint32_t ct_validate(const tb_transfer_t& t) {
   const u128 dr = U(t.debit_account_id), cr = U(t.credit_account_id);
   if (dr == 0) return TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
   if (dr == MAX128) return TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
@@ -33,14 +33,14 @@ __device__ inline uint32_t ct_validate(const tb_transfer_t& t) {
 }
 
 // Ledger checks once both accounts are found (:1503-1504).
-__device__ inline uint32_t ct_ledgers(const tb_transfer_t& t, uint32_t dr_ledger, uint32_t cr_ledger) {
+__device__ __attribute__((always_inline)) inline uint32_t ct_ledgers(const tb_transfer_t& t, uint32_t dr_ledger, uint32_t cr_ledger) {
   if (dr_ledger != cr_ledger) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
   if (t.ledger != dr_ledger) return TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
   return CONT;
 }
 
 // create_transfer_exists (:1587-1606).
-__device__ inline uint32_t ct_exists(const tb_transfer_t& t, const tb_transfer_t& e) {
+__device__ __attribute__((always_inline)) inline uint32_t ct_exists(const tb_transfer_t& t, const tb_transfer_t& e) {
   if (t.flags != e.flags) return TB_CT_EXISTS_WITH_DIFFERENT_FLAGS;
   if (U(t.debit_account_id) != U(e.debit_account_id)) return TB_CT_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
   if (U(t.credit_account_id) != U(e.credit_account_id)) return TB_CT_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
@@ -54,7 +54,7 @@ __device__ inline uint32_t ct_exists(const tb_transfer_t& t, const tb_transfer_t
 }
 
 // post_or_void_pending_transfer steps before the pending lookup (:1614-1624).
-__device__ inline uint32_t pv_validate(const tb_transfer_t& t) {
+__device__ __attribute__((always_inline)) inline uint32_t pv_validate(const tb_transfer_t& t) {
   const uint16_t f = t.flags;
   if ((f & TB_TRANSFER_POST_PENDING) && (f & TB_TRANSFER_VOID_PENDING)) return TB_CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
   if (f & TB_TRANSFER_PENDING) return TB_CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
@@ -70,7 +70,7 @@ __device__ inline uint32_t pv_validate(const tb_transfer_t& t) {
 
 // Checks against the found pending transfer p, up to (excluding) the exists check (:1629-1654).
 // Outputs the posted/voided amount.
-__device__ inline uint32_t pv_against(const tb_transfer_t& t, const tb_transfer_t& p, u128* amount_out) {
+__device__ __attribute__((always_inline)) inline uint32_t pv_against(const tb_transfer_t& t, const tb_transfer_t& p, u128* amount_out) {
   if (!(p.flags & TB_TRANSFER_PENDING)) return TB_CT_PENDING_TRANSFER_NOT_PENDING;
   const u128 tdr = U(t.debit_account_id), tcr = U(t.credit_account_id);
   if (tdr > 0 && tdr != U(p.debit_account_id)) return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID;
@@ -86,7 +86,7 @@ __device__ inline uint32_t pv_against(const tb_transfer_t& t, const tb_transfer_
 }
 
 // post_or_void_pending_transfer_exists (:1743-1804).
-__device__ inline uint32_t pv_exists(const tb_transfer_t& t, const tb_transfer_t& e, const tb_transfer_t& p) {
+__device__ __attribute__((always_inline)) inline uint32_t pv_exists(const tb_transfer_t& t, const tb_transfer_t& e, const tb_transfer_t& p) {
   if (t.flags != e.flags) return TB_CT_EXISTS_WITH_DIFFERENT_FLAGS;
   if (U(t.amount) == 0) {
     if (U(e.amount) != U(p.amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
@@ -113,7 +113,7 @@ __device__ inline uint32_t pv_exists(const tb_transfer_t& t, const tb_transfer_t
 }
 
 // Pending status switch (:1658-1670).
-__device__ inline uint32_t pv_status(uint8_t status) {
+__device__ __attribute__((always_inline)) inline uint32_t pv_status(uint8_t status) {
   switch (status) {
     case TB_PENDING_POSTED: return TB_CT_PENDING_TRANSFER_ALREADY_POSTED;
     case TB_PENDING_VOIDED: return TB_CT_PENDING_TRANSFER_ALREADY_VOIDED;
@@ -123,7 +123,7 @@ __device__ inline uint32_t pv_status(uint8_t status) {
 }
 
 // The posting/voiding transfer record that post_or_void inserts (:1672-1686).
-__device__ inline tb_transfer_t pv_record(const tb_transfer_t& t, const tb_transfer_t& p, u128 amount) {
+__device__ __attribute__((always_inline)) inline tb_transfer_t pv_record(const tb_transfer_t& t, const tb_transfer_t& p, u128 amount) {
   tb_transfer_t t2;
   t2.id = t.id;
   t2.debit_account_id = p.debit_account_id;
@@ -141,14 +141,14 @@ __device__ inline tb_transfer_t pv_record(const tb_transfer_t& t, const tb_trans
   return t2;
 }
 
-__device__ inline uint64_t expires_at_of(const tb_transfer_t& p) {
+__device__ __attribute__((always_inline)) inline uint64_t expires_at_of(const tb_transfer_t& p) {
   return p.timestamp + (uint64_t)p.timeout * TB_NS_PER_S;
 }
 
 struct Bal {
   u128 dp, dpo, cp, cpo;
 };
-__device__ inline Bal load_bal(const tb_account_t* a) {
+__device__ __attribute__((always_inline)) inline Bal load_bal(const tb_account_t* a) {
   Bal b;
   b.dp = U(a->debits_pending);
   b.dpo = U(a->debits_posted);
@@ -156,7 +156,7 @@ __device__ inline Bal load_bal(const tb_account_t* a) {
   b.cpo = U(a->credits_posted);
   return b;
 }
-__device__ inline void store_bal(tb_account_t* a, const Bal& b) {
+__device__ __attribute__((always_inline)) inline void store_bal(tb_account_t* a, const Bal& b) {
   a->debits_pending = W(b.dp);
   a->debits_posted = W(b.dpo);
   a->credits_pending = W(b.cp);
@@ -165,7 +165,7 @@ __device__ inline void store_bal(tb_account_t* a, const Bal& b) {
 
 // Balance-dependent tail of create_transfer (:1509-1547): balancing clamp, overflow checks,
 // timeout overflow, limits. Returns OK with the (clamped) amount, or the failing code.
-__device__ inline uint32_t ct_balances(const tb_transfer_t& t, const Bal& dr, uint16_t dr_flags, const Bal& cr,
+__device__ __attribute__((always_inline)) inline uint32_t ct_balances(const tb_transfer_t& t, const Bal& dr, uint16_t dr_flags, const Bal& cr,
                                        uint16_t cr_flags, u128* amount_out) {
   const uint16_t f = t.flags;
   const bool bdr = f & TB_TRANSFER_BALANCING_DEBIT, bcr = f & TB_TRANSFER_BALANCING_CREDIT;
@@ -201,7 +201,7 @@ __device__ inline uint32_t ct_balances(const tb_transfer_t& t, const Bal& dr, ui
 }
 
 // create_account validation (state_machine.zig:1424-1439).
-__device__ inline uint32_t ca_validate(const tb_account_t& a) {
+__device__ __attribute__((always_inline)) inline uint32_t ca_validate(const tb_account_t& a) {
   if (a.reserved != 0) return TB_CA_RESERVED_FIELD;
   if (a.flags & TB_ACCOUNT_PADDING_MASK) return TB_CA_RESERVED_FLAG;
   const u128 id = U(a.id);
@@ -219,7 +219,7 @@ __device__ inline uint32_t ca_validate(const tb_account_t& a) {
 }
 
 // create_account_exists (:1450-1460). Compares the whole u16 flags, linked included.
-__device__ inline uint32_t ca_exists(const tb_account_t& a, const tb_account_t& e) {
+__device__ __attribute__((always_inline)) inline uint32_t ca_exists(const tb_account_t& a, const tb_account_t& e) {
   if (a.flags != e.flags) return TB_CA_EXISTS_WITH_DIFFERENT_FLAGS;
   if (U(a.user_data_128) != U(e.user_data_128)) return TB_CA_EXISTS_WITH_DIFFERENT_USER_DATA_128;
   if (a.user_data_64 != e.user_data_64) return TB_CA_EXISTS_WITH_DIFFERENT_USER_DATA_64;

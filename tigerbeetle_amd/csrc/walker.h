@@ -75,6 +75,12 @@ __device__ inline void bmap_set_committed(BEntry* bm, uint32_t e, uint32_t epoch
   bm[e].commit = ((unsigned long long)epoch << 32) | (uint32_t)i;
 }
 
+// An event's static inputs (written by k_ct_prep / k_classify before any walker runs, never by a
+// walker for a later event), loaded one event ahead so the walk pays only its dynamic reads.
+struct WPre {
+  uint32_t i, cls, b, code, id_tslot, id_ent, dr, cr, p_tslot, pid_ent;
+};
+
 struct Walker {
   Dev d;
   Scratch s;
@@ -93,7 +99,7 @@ struct Walker {
   // the low word) and no walker waits for an atomic's result.
   bool small_bal = false;
 
-  __device__ void log_bal(uint32_t slot) {
+  __device__ __attribute__((always_inline)) void log_bal(uint32_t slot) {
     if (!scope) return;
     UndoRec& r = s.undo[undo_n++];
     r.kind = UNDO_BAL;
@@ -104,7 +110,7 @@ struct Walker {
     r.old[2] = b.cp;
     r.old[3] = b.cpo;
   }
-  __device__ void log_small(uint32_t kind, uint32_t a, u128 old) {
+  __device__ __attribute__((always_inline)) void log_small(uint32_t kind, uint32_t a, u128 old) {
     if (!scope) return;
     UndoRec& r = s.undo[undo_n++];
     r.kind = kind;
@@ -114,7 +120,7 @@ struct Walker {
   __device__ static tb_uint128_t* bal_field(tb_account_t* a, uint32_t f) {
     return f == 0 ? &a->debits_pending : f == 1 ? &a->debits_posted : f == 2 ? &a->credits_pending : &a->credits_posted;
   }
-  __device__ void add_bal(uint32_t slot, uint32_t f, u128 v) {
+  __device__ __attribute__((always_inline)) void add_bal(uint32_t slot, uint32_t f, u128 v) {
     if (small_bal)
       (void)atomicAdd(reinterpret_cast<unsigned long long*>(bal_field(&d.acc[slot], f)), (unsigned long long)v);
     else
@@ -126,7 +132,7 @@ struct Walker {
     r.pad0 = f;
     r.old[0] = v;
   }
-  __device__ void rollback() {
+  __device__ __attribute__((always_inline)) void rollback() {
     while (undo_n) {
       const UndoRec& r = s.undo[--undo_n];
       switch (r.kind) {
@@ -155,7 +161,7 @@ struct Walker {
 
   // historical_balance (:1806-1841): the row of event i from the accounts' balances after it
   // (sequential mode only: windows with history accounts never run component walkers)
-  __device__ void history(uint32_t i, uint32_t drs, const Bal& dr, uint32_t crs, const Bal& cr) {
+  __device__ __attribute__((always_inline)) void history(uint32_t i, uint32_t drs, const Bal& dr, uint32_t crs, const Bal& cr) {
     const uint16_t fd = d.acc[drs].flags, fc = d.acc[crs].flags;
     if (!((fd | fc) & TB_ACCOUNT_HISTORY)) return;
     HistRow r;
@@ -173,7 +179,7 @@ struct Walker {
     s.hside[i] = side;
   }
 
-  __device__ void commit_record(uint32_t i, const tb_transfer_t& t2) {
+  __device__ __attribute__((always_inline)) void commit_record(uint32_t i, const tb_transfer_t& t2) {
     s.t2[i] = t2;
     s.hside[i] = 0;
     log_small(UNDO_INS, i, 0);
@@ -183,22 +189,52 @@ struct Walker {
     bmap_set_committed(s.bmap, e, epoch, (int32_t)i);
   }
 
+  template <bool XFER>
+  __device__ __attribute__((always_inline)) WPre fetch(uint32_t i) {
+    WPre e;
+    e.i = i;
+    e.cls = s.cls[i];
+    e.b = s.batch[i];
+    e.code = s.code[i];
+    e.id_tslot = s.id_tslot[i];
+    e.id_ent = s.id_ent[i];
+    if (XFER) {
+      e.dr = s.dr_slot[i];
+      e.cr = s.cr_slot[i];
+      e.p_tslot = s.p_tslot[i];
+      e.pid_ent = s.pid_ent[i];
+    }
+    return e;
+  }
+
   // create_transfer (:1462-1585) from the exists check on; validation results come from k_ct_prep.
-  __device__ uint32_t transfer(uint32_t i, uint32_t cls) {
-    if (cls & C_STATIC) return s.code[i];
+  __device__ __attribute__((always_inline)) uint32_t transfer(const WPre& e) {
+    const uint32_t i = e.i;
+    if (e.cls & C_STATIC) return e.code;
     tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev)[i];
-    t.timestamp = win_ts(*w, s.batch[i], i);
-    if (cls & C_POSTVOID) return post_or_void(i, t);
-    if (s.id_tslot[i] != NONE32) return ct_exists(t, d.xr[s.id_tslot[i]]);
-    const int32_t c = bmap_committed(s.bmap, s.id_ent[i], epoch);
+    t.timestamp = win_ts(*w, e.b, i);
+    if (e.cls & C_POSTVOID) return post_or_void(e, t);
+    if (e.id_tslot != NONE32) return ct_exists(t, d.xr[e.id_tslot]);
+    const int32_t c = bmap_committed(s.bmap, e.id_ent, epoch);
     if (c >= 0) return ct_exists(t, s.t2[c]);
-    const uint32_t drs = s.dr_slot[i], crs = s.cr_slot[i];
+    const uint32_t drs = e.dr, crs = e.cr;
     tb_account_t* dra = &d.acc[drs];
     tb_account_t* cra = &d.acc[crs];
-    Bal dr = load_bal(dra), cr = load_bal(cra);
     u128 amount;
-    const uint32_t r = ct_balances(t, dr, dra->flags, cr, cra->flags, &amount);
-    if (r != TB_CT_OK) return r;
+    if (atomic_bal) {
+      // No decision of this window reads a balance (no event has C_READS_*: no limit flag on its
+      // accounts, no balancing) and it is overflow-free: the checks see zero balances the same way.
+      const Bal z = {0, 0, 0, 0};
+      const uint32_t r = ct_balances(t, z, 0, z, 0, &amount);
+      if (r != TB_CT_OK) return r;
+    }
+    Bal dr, cr;
+    if (!atomic_bal) {
+      dr = load_bal(dra);
+      cr = load_bal(cra);
+      const uint32_t r = ct_balances(t, dr, dra->flags, cr, cra->flags, &amount);
+      if (r != TB_CT_OK) return r;
+    }
     t.amount = W(amount);
     commit_record(i, t);
     if (atomic_bal) {
@@ -225,27 +261,29 @@ struct Walker {
   }
 
   // post_or_void_pending_transfer (:1608-1741) from the pending lookup on.
-  __device__ uint32_t post_or_void(uint32_t i, const tb_transfer_t& t) {
-    const uint32_t pslot = s.p_tslot[i];
+  __device__ __attribute__((always_inline)) uint32_t post_or_void(const WPre& e, const tb_transfer_t& t) {
+    const uint32_t i = e.i;
+    const uint32_t pslot = e.p_tslot;
     int32_t pc = -1;
     uint32_t drs, crs;
-    tb_transfer_t p;
+    const tb_transfer_t* pp;  // one load from the selected record (no merged aggregate)
     if (pslot != NONE32) {
-      p = d.xr[pslot];
-      drs = s.dr_slot[i];
-      crs = s.cr_slot[i];
+      pp = &d.xr[pslot];
+      drs = e.dr;
+      crs = e.cr;
     } else {
-      pc = bmap_committed(s.bmap, s.pid_ent[i], epoch);
+      pc = bmap_committed(s.bmap, e.pid_ent, epoch);
       if (pc < 0) return TB_CT_PENDING_TRANSFER_NOT_FOUND;
-      p = s.t2[pc];
+      pp = &s.t2[pc];
       drs = s.dr_slot[pc];
       crs = s.cr_slot[pc];
     }
+    const tb_transfer_t p = *pp;
     u128 amount;
     uint32_t r = pv_against(t, p, &amount);
     if (r != CONT) return r;
-    if (s.id_tslot[i] != NONE32) return pv_exists(t, d.xr[s.id_tslot[i]], p);
-    const int32_t c = bmap_committed(s.bmap, s.id_ent[i], epoch);
+    if (e.id_tslot != NONE32) return pv_exists(t, d.xr[e.id_tslot], p);
+    const int32_t c = bmap_committed(s.bmap, e.id_ent, epoch);
     if (c >= 0) return pv_exists(t, s.t2[c], p);
     uint8_t pst = pc >= 0 ? s.bstatus[pc] : d.xstatus[pslot];
     if (pst == TB_PENDING_PENDING && xw_expired_before(*w, p, s.batch[i])) pst = TB_PENDING_EXPIRED;
@@ -299,7 +337,7 @@ struct Walker {
   }
 
   // create_account (:1421-1448) from the exists check on.
-  __device__ uint32_t account(uint32_t i, uint32_t cls) {
+  __device__ __attribute__((always_inline)) uint32_t account(uint32_t i, uint32_t cls) {
     if (cls & C_STATIC) return s.code[i];
     if (s.id_tslot[i] != NONE32) return s.code[i];  // exists before the window: static
     const tb_account_t* evs = reinterpret_cast<const tb_account_t*>(ev);
@@ -315,16 +353,27 @@ struct Walker {
 
   // Walks the events list[0..count) (ascending window positions).
   template <bool XFER>
-  __device__ void run(const uint32_t* list, uint32_t count) {
+  __device__ __attribute__((always_inline)) void run(const uint32_t* list, uint32_t count) {
     int32_t chain = -1;
     bool broken = false;
     undo_n = 0;
     scope = false;
+    // software pipeline: event k + 1's static inputs load while event k runs; list[k + 2] one
+    // step earlier still
+    WPre nx;
+    uint32_t i2 = NONE32;
+    if (count) nx = fetch<XFER>(list[0]);
+    if (count > 1) i2 = list[1];
     for (uint32_t k = 0; k < count; k++) {
-      const uint32_t i = list[k];
-      const uint32_t cls = s.cls[i];
+      const WPre cur = nx;
+      if (k + 1 < count) {
+        nx = fetch<XFER>(i2);
+        if (k + 2 < count) i2 = list[k + 2];
+      }
+      const uint32_t i = cur.i;
+      const uint32_t cls = cur.cls;
       const bool linked = cls & C_LINKED;
-      const uint32_t b = s.batch[i];
+      const uint32_t b = cur.b;
       uint32_t r;
       if (linked && chain < 0) {
         chain = (int32_t)i;
@@ -338,7 +387,7 @@ struct Walker {
       } else if (cls & C_TSNZ) {
         r = TB_CT_TIMESTAMP_MUST_BE_ZERO;
       } else {
-        r = XFER ? transfer(i, cls) : account(i, cls);
+        r = XFER ? transfer(cur) : account(i, cls);
       }
       if (r != TB_CT_OK && chain >= 0 && !broken) {
         broken = true;

@@ -14,6 +14,7 @@ struct WinDesc {
   uint32_t E;              // events in the window
   uint32_t off[MAXB + 1];  // event offset of each batch; off[nb] = E
   uint32_t xwin;           // pulses inside the window are modelled (xwin.h): it spans >= 1 s
+  uint32_t log;            // TBG_WINDOW_LOG: batches from a replica's log, no pulse between them
   uint64_t T[MAXB];        // commit timestamp of each batch
 };
 

@@ -220,3 +220,17 @@ class StateMachine:
         a, s = ctypes.c_uint64(), ctypes.c_uint64()
         _lib.check(_lib.lib().tbg_windows_committed(self.h, ctypes.byref(a), ctypes.byref(s)), "windows_committed")
         return a.value, s.value
+
+    def aof_replay(self, data, flags=0):
+        """tbg_aof_replay: applies an AOF file's prepares (bytes / uint8 array, e.g. np.memmap) in
+        order, every checksum verified on the GPU. Returns the stats as a dict; `error` names the
+        AOF.Iterator error at `error_entry` (the entries before it are applied) or is None."""
+        buf = np.ascontiguousarray(np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else data)
+        st = _lib.AofStats()
+        rc = _lib.lib().tbg_aof_replay(self.h, buf.ctypes.data if buf.size else None, buf.size, flags,
+                                       ctypes.byref(st))
+        if rc not in (0, -1) or (rc == -1 and st.error == 0):
+            _lib.check(rc, "aof_replay")
+        out = {k: getattr(st, k) for k, _ in _lib.AofStats._fields_ if k != "reserved"}
+        out["error"] = _lib.AOF_ERRORS[st.error]
+        return out
