@@ -257,6 +257,33 @@ typedef struct tbg_aof_stats {
 } tbg_aof_stats;
 int tbg_aof_replay(tbg_engine *engine, const void *h_aof, uint64_t size, uint32_t flags, tbg_aof_stats *stats);
 
+/* Sharded engines, general class (tigerbeetle_amd/csrc/shard_gx.inc): a batch outside the
+ * order-free class (balance limits, balancing, two-phase, in-window duplicate ids) or with a pulse
+ * due before it is decided on every shard identically from its gathered read set:
+ *   tbg_shard_gather(phase 1), sum across the shards, tbg_shard_gather(phase 2) into the buffer's
+ *   second region, sum that region, then every shard opens its scratch unsharded engine from the
+ *   gathered objects (tbg_reset + tbg_open_device, the shards' common pulse_next_timestamp),
+ *   commits the batch there with its pulse (tbg_commit_window, auto_pulse), and applies the
+ *   post-batch objects it owns (tbg_device_state of the scratch engine -> tbg_shard_apply).
+ * The buffer (tbg_shard_gather_bytes, 256-byte aligned) holds one writer per slot, so its byte-wise
+ * sum is the union. The C-ABI steps are device work on the engine stream; the Python driver
+ * (tigerbeetle_amd/sharding.py) dedupes and orders the gathered objects. */
+uint64_t tbg_shard_gather_bytes(uint32_t n_events, uint32_t shard_count, uint32_t batch_max, uint64_t *phase2_offset);
+int tbg_shard_gather(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_events,
+                     uint64_t timestamp, uint32_t phase, void *d_buffer);
+int tbg_shard_apply(tbg_engine *engine, const tb_account_t *d_accounts, uint64_t n_accounts,
+                    const tb_transfer_t *d_transfers, const uint8_t *d_status, uint64_t n_transfers,
+                    uint64_t pulse_next_timestamp);
+/* Unsharded engines: open (as tbg_open) from device-resident objects in timestamp order with the
+ * given pulse_next_timestamp; and the device view of the whole state (valid until the next call
+ * that changes it). */
+int tbg_open_device(tbg_engine *engine, const tb_account_t *d_accounts, uint64_t n_accounts,
+                    const tb_transfer_t *d_transfers, const uint8_t *d_status, uint64_t n_transfers,
+                    uint64_t pulse_next_timestamp);
+int tbg_device_state(tbg_engine *engine, const tb_account_t **accounts, uint64_t *n_accounts,
+                     const tb_transfer_t **transfers, const uint8_t **status, uint64_t *n_transfers,
+                     uint64_t *pulse_next_timestamp);
+
 /* Test hook mirroring the harness `setup` action (state_machine.zig:2545-2561). */
 int tbg_setup_balances(tbg_engine *engine, const tb_uint128_t *id, const tb_uint128_t *debits_pending,
                        const tb_uint128_t *debits_posted, const tb_uint128_t *credits_pending,

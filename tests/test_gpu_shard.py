@@ -31,6 +31,51 @@ class LocalShards:
         for s in self.shards:
             s.close()
 
+    def summed(self, tensors):
+        """The exchange, in-process: every tensor becomes the sum of all of them."""
+        import torch
+
+        for s in self.shards:  # engine streams are non-blocking: wait for each explicitly
+            s.stream.synchronize()
+        total = tensors[0].clone()
+        for t in tensors[1:]:
+            total += t
+        for t in tensors:
+            t.copy_(total)
+        torch.cuda.synchronize()
+
+    def commit_any(self, op, batches, tick_ns=0):
+        """A window through the order-free path when no pulse can be due in it, else (or when the
+        window is outside the order-free class) batch by batch through the general path
+        (csrc/shard_gx.inc). Returns (per-batch replies, took the fast path)."""
+        import torch
+
+        from tigerbeetle_amd._lib import UnsupportedWindow
+        from tigerbeetle_amd.sharding import commit_general_batch
+
+        ts0 = self.prepare_timestamp
+        t_last = ts0 + tick_ns + sum(1 + len(ev) for ev in batches)
+        if t_last < self.shards[0].pulse_next():
+            try:
+                return self.commit_window(op, batches, tick_ns), True
+            except UnsupportedWindow:
+                for s in self.shards:  # every shard reports the rejected window once
+                    try:
+                        s.sync()
+                    except UnsupportedWindow:
+                        pass
+                self.prepare_timestamp = ts0
+        out = []
+        self.prepare_timestamp = ts0 + tick_ns
+        for ev in batches:
+            self.prepare_timestamp += 1 + len(ev)
+            data = np.frombuffer(ev.tobytes(), np.uint8)
+            d_ev = torch.from_numpy(data.copy()).cuda() if len(data) else torch.zeros(128, dtype=torch.uint8).cuda()
+            torch.cuda.synchronize()
+            out.append(commit_general_batch(self.shards, self.summed, op, d_ev.data_ptr(), len(ev),
+                                            self.prepare_timestamp))
+        return out, False
+
     def commit_window(self, op, batches, tick_ns=0):
         """The five steps of csrc/shard.h with both exchanges summed in-process; returns the per-batch
         replies assembled from every shard's home batches."""
@@ -46,16 +91,7 @@ class LocalShards:
         d_ev = torch.from_numpy(data.copy()).cuda() if len(data) else torch.zeros(128, dtype=torch.uint8).cuda()
         torch.cuda.synchronize()
 
-        def summed(tensors):
-            for s in self.shards:  # engine streams are non-blocking: wait for each explicitly
-                s.stream.synchronize()
-            total = tensors[0].clone()
-            for t in tensors[1:]:
-                total += t
-            for t in tensors:
-                t.copy_(total)
-            torch.cuda.synchronize()
-
+        summed = self.summed
         summed([s.prepare_window(op, d_ev.data_ptr(), ns, ts) for s in self.shards])
         outs, bits = [], []
         for s in self.shards:

@@ -1,0 +1,169 @@
+"""Hash-sharded engine, general class (csrc/shard_gx.inc): balance limits and balancing
+(the interleaved debit / credit checks of state_machine.zig:1509-1547), two-phase with timeouts
+(:1608-1741), in-window duplicate ids, and the pulses (:1874-1929, :2018-2173) on shards. Windows
+the order-free path can take still take it; the others go batch by batch through the gathered read
+set and the scratch engine. Against the CPU restatement batch by batch under the harness protocol:
+every reply, pulse_next_timestamp after every window, and the union of the shards' stores and
+TransferPending statuses, each record on the shard its id hashes to."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from chaos import Chaos, run_protocol
+from oracle_sm import OracleStateMachine
+from test_gpu_shard import LocalShards, _compare_sharded
+from test_gpu_window import oracle_batches
+from tigerbeetle_amd import workload
+from tigerbeetle_amd.types import NS_PER_S, Operation
+
+
+def _statuses(sh):
+    rows = []
+    for s in sh.shards:
+        t = s.sm.dump_transfers()
+        rows.append((t["timestamp"], s.sm.dump_transfer_status()))
+    ts = np.concatenate([r[0] for r in rows])
+    st = np.concatenate([r[1] for r in rows])
+    return st[np.argsort(ts, kind="stable")]
+
+
+def _check(sh, ref):
+    _compare_sharded(sh, ref)
+    assert _statuses(sh).tobytes() == ref.dump_transfer_status().tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,seed,win,bm", [(2, 0, 4, 16), (3, 1, 3, 32), (8, 2, 4, 16), (4, 3, 2, 64)])
+def test_shard_general_chaos(G, seed, win, bm):
+    """Chaos streams (limits, balancing, two-phase with 1-9 s timeouts, posts/voids, chains with
+    rollback, duplicate ids in and across windows, invalid fields) with clock ticks, interleaved with
+    plain uniform windows (the order-free path)."""
+    sh = LocalShards(G, bm, 4096, 1 << 16, win * bm)
+    ref = OracleStateMachine(batch_max=bm)
+    ch = Chaos(7000 + seed, n_accounts=30)
+    fast = general = 0
+    try:
+        for w in range(26):
+            if w == 0 or w % 5 == 4:
+                op = Operation.create_accounts  # fresh unique valid accounts: the order-free class
+                batches = [workload.accounts(10**6 + w * 10**4 + k * bm, ch.rng.randint(1, bm), seed=w)
+                           for k in range(win)]
+            elif w == 1:
+                op = Operation.create_accounts
+                batches = [ch.accounts_batch(ch.rng.randint(1, bm)) for _ in range(win)]
+            else:
+                op = Operation.create_transfers
+                batches = [ch.transfers_batch(ch.rng.choice([1, 3, bm // 2, bm])) for _ in range(win)]
+            tick = 0 if op == Operation.create_accounts else ch.rng.choice([0, 0, NS_PER_S, 2 * NS_PER_S])
+            g, took_fast = sh.commit_any(op, batches, tick)
+            r = oracle_batches(ref, op, batches, tick)
+            assert g == r, f"window {w} (fast={took_fast})"
+            assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp(), f"window {w}"
+            fast += int(took_fast)
+            general += int(not took_fast)
+        _check(sh, ref)
+        assert fast > 0 and general > 0, (fast, general)
+    finally:
+        sh.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_shard_general_expiry_cap():
+    """More transfers due at once than a pulse may expire (batch_max): each shard offers its
+    cap + 1 smallest, the scratch engine selects the global cap smallest, the rest follow in later
+    pulses."""
+    G, bm = 3, 8
+    sh = LocalShards(G, bm, 1024, 1 << 14, bm)
+    ref = OracleStateMachine(batch_max=bm)
+    ch = Chaos(7100, n_accounts=10, pending=0.9, postvoid=0.05, limits=0.0, balancing=0.0, linked=0.05, invalid=0.0)
+    try:
+        for b in range(40):
+            if b < 2:
+                ev, op = ch.accounts_batch(bm), Operation.create_accounts
+            else:
+                ev, op = ch.transfers_batch(bm), Operation.create_transfers
+            tick = 5 * NS_PER_S if b % 8 == 7 else 0
+            g, _ = sh.commit_any(op, [ev], tick)
+            assert g == [run_protocol(ref, op, ev, tick)], f"batch {b}"
+            assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp()
+        _check(sh, ref)
+        assert (ref.dump_transfer_status() == 4).sum() > bm  # expired, over several capped pulses
+    finally:
+        sh.close()
+        ref.close()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _dist_stream(seed, bm):
+    ch = Chaos(seed, n_accounts=20)
+    out = []
+    for b in range(30):
+        if b < 2:
+            out.append((Operation.create_accounts, ch.accounts_batch(bm), 0))
+        else:
+            out.append((Operation.create_transfers, ch.transfers_batch(ch.rng.choice([1, bm // 2, bm])),
+                        ch.rng.choice([0, NS_PER_S])))
+    return out
+
+
+def _rank_main(rank, world, port, seed, bm, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tigerbeetle_amd.sharding import ShardedStateMachine, exchange_gloo
+
+    sh = ShardedStateMachine(world, rank, exchange_gloo, batch_max=bm, accounts_max=1024, transfers_max=1 << 14,
+                             window_events_max=bm)
+    ts, replies = 0, []
+    for op, ev, tick in _dist_stream(seed, bm):
+        ts += tick + 1 + len(ev)
+        d_ev = torch.from_numpy(np.frombuffer(ev.tobytes(), np.uint8).copy()).cuda()
+        torch.cuda.synchronize()
+        replies.append(sh.commit_general(op, d_ev.data_ptr(), len(ev), ts).hex())
+    np.save(os.path.join(out_dir, f"acc{rank}.npy"), sh.sm.dump_accounts())
+    np.save(os.path.join(out_dir, f"xfer{rank}.npy"), sh.sm.dump_transfers())
+    np.save(os.path.join(out_dir, f"st{rank}.npy"), sh.sm.dump_transfer_status())
+    import json
+
+    with open(os.path.join(out_dir, f"rep{rank}.json"), "w") as f:
+        json.dump(replies, f)
+    sh.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_shard_general_two_rank_gloo(tmp_path):
+    """Two processes (one shard each, sharing cuda:0), every exchange a torch.distributed
+    all-reduce: each rank returns every batch's reply, equal to the restatement's."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    world, seed, bm = 2, 7200, 16
+    mp.spawn(_rank_main, args=(world, _free_port(), seed, bm, str(tmp_path)), nprocs=world, join=True)
+    ref = OracleStateMachine(batch_max=bm)
+    try:
+        expect = [run_protocol(ref, op, ev, tick).hex() for op, ev, tick in _dist_stream(seed, bm)]
+        for r in range(world):
+            with open(tmp_path / f"rep{r}.json") as f:
+                assert json.load(f) == expect
+        acc = np.concatenate([np.load(tmp_path / f"acc{r}.npy") for r in range(world)])
+        xfer = np.concatenate([np.load(tmp_path / f"xfer{r}.npy") for r in range(world)])
+        st = np.concatenate([np.load(tmp_path / f"st{r}.npy") for r in range(world)])
+        o = np.argsort(xfer["timestamp"], kind="stable")
+        assert acc[np.argsort(acc["timestamp"], kind="stable")].tobytes() == ref.dump_accounts().tobytes()
+        assert xfer[o].tobytes() == ref.dump_transfers().tobytes()
+        assert st[o].tobytes() == ref.dump_transfer_status().tobytes()
+    finally:
+        ref.close()

@@ -20,7 +20,8 @@ EXPORTS = [
     "tbg_shard_commit_bits_bytes", "tbg_window_changes", "tbg_windows_committed",
     "tbg_open", "tbg_reset", "tbg_prefetch_poll", "tbg_compact", "tbg_checkpoint", "tbg_digest",
     "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free", "tbg_checksum",
-    "tbg_demux_init", "tbg_demux_decode", "tbg_aof_replay",
+    "tbg_demux_init", "tbg_demux_decode", "tbg_aof_replay", "tbg_shard_gather_bytes", "tbg_shard_gather",
+    "tbg_shard_apply", "tbg_open_device", "tbg_device_state",
 ]
 
 
@@ -139,6 +140,11 @@ def lib():
         "tbg_demux_init": ([P(Demuxer), u32, vp, u32], i32),
         "tbg_demux_decode": ([P(Demuxer), u32, u32, P(vp), P(u32)], i32),
         "tbg_aof_replay": ([vp, vp, u64, u32, P(AofStats)], i32),
+        "tbg_shard_gather_bytes": ([u32, u32, u32, P(u64)], u64),
+        "tbg_shard_gather": ([vp, u32, vp, u32, u64, u32, vp], i32),
+        "tbg_shard_apply": ([vp, vp, u64, vp, vp, u64, u64], i32),
+        "tbg_open_device": ([vp, vp, u64, vp, vp, u64, u64], i32),
+        "tbg_device_state": ([vp, P(vp), P(u64), P(vp), P(vp), P(u64), P(u64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

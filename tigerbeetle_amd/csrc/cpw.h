@@ -77,12 +77,23 @@ __global__ void __launch_bounds__(256) k_cc_keys(Dev d, Scratch s, uint32_t E) {
 }
 
 // Component starts in the sorted order.
+// (one counter atomic per wave: ~140K component starts per cfg4 window would serialize on it)
 __global__ void __launch_bounds__(256) k_cc_segs(Dev d, Scratch s, uint32_t E) {
+  if (!cpw_active(d.g)) return;
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= E || !cpw_active(d.g)) return;
-  const uint32_t key = s.rkey[k];
-  if (key == RES_DUMMY || (k > 0 && s.rkey[k - 1] == key)) return;
-  s.cc_list[atomicAdd(&d.g->cc_count, 1u)] = k;
+  bool start = false;
+  if (k < E) {
+    const uint32_t key = s.rkey[k];
+    start = key != RES_DUMMY && (k == 0 || s.rkey[k - 1] != key);
+  }
+  const unsigned long long m = __ballot(start);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(&d.g->cc_count, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (start) s.cc_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = k;
 }
 
 // One walker per component: events rval[start .. start + len), undo records from 5 * start.

@@ -24,6 +24,7 @@ import numpy as np
 
 from . import _lib
 from .state_machine import StateMachine
+from .types import Operation
 
 _M1, _M2 = np.uint64(0xFF51AFD7ED558CCD), np.uint64(0xC4CEB9FE1A85EC53)
 
@@ -86,6 +87,8 @@ class ShardedStateMachine:
                                transfers_max=transfers_max, window_events_max=window_events_max,
                                shard_count=shard_count, shard_index=shard_index)
         self.shard_count, self.shard_index = shard_count, shard_index
+        self.batch_max, self.device = batch_max, device
+        self.scratch = None
         self.exchange = exchange
         events_max = window_events_max or batch_max
         dev = torch.device("cuda", device)
@@ -100,6 +103,8 @@ class ShardedStateMachine:
         return self.sm.h
 
     def close(self):
+        if self.scratch is not None:
+            self.scratch.close()
         self.sm.close()
 
     def home_range(self, n_batches):
@@ -150,3 +155,140 @@ class ShardedStateMachine:
 
     def stats(self):
         return self.sm.stats()
+
+    # --------------------------------------------------------------------------------------------
+    # General class (csrc/shard_gx.inc): one batch at a time, decided on every shard from the
+    # gathered read set by a scratch unsharded engine.
+    # --------------------------------------------------------------------------------------------
+    def pulse_next(self):
+        """pulse_next_timestamp, the same on every shard."""
+        return self.sm.stats()["pulse_next_timestamp"]
+
+    def _gx_init(self):
+        import torch
+
+        if getattr(self, "scratch", None) is not None:
+            return
+        bm, G = self.batch_max, self.shard_count
+        C = bm + 1
+        dev = torch.device("cuda", self.device)
+        self.gx = torch.zeros(_gx_layout(bm, G, C)["bytes"], dtype=torch.uint8, device=dev)
+        self.scratch = StateMachine(device=self.device, batch_max=bm, accounts_max=4 * bm + 2 * G * C + 64,
+                                    transfers_max=3 * bm + G * C + G + 64, window_events_max=bm)
+        self.gx_res = torch.zeros(max(bm, 1) * 8, dtype=torch.uint8, device=dev)
+        self.gx_base = torch.zeros(2, dtype=torch.int32, device=dev)
+
+    def gather(self, operation, d_events, n, timestamp, phase):
+        """Gather phase 1 or 2 of one batch; returns the region to be summed across the shards."""
+        import torch
+
+        self._gx_init()
+        lay = _gx_layout(n, self.shard_count, self.batch_max + 1)
+        _lib.check(_lib.lib().tbg_shard_gather(self.sm.h, int(operation), d_events, n, timestamp, phase,
+                                               self.gx.data_ptr()), "shard_gather")
+        torch.cuda.synchronize(self.device)
+        return self.gx[: lay["p2"]] if phase == 1 else self.gx[lay["p2"]: lay["bytes"]]
+
+    def commit_general(self, operation, d_events, n, timestamp):
+        """One batch (its harness pulse included) through the general path with this process's
+        exchange; every shard returns the batch's whole reply."""
+        def summed(tensors):
+            if self.exchange is not None:
+                for t in tensors:
+                    self.exchange(t)
+
+        return commit_general_batch([self], summed, operation, d_events, n, timestamp)
+
+    def decide_apply(self, operation, d_events, n, timestamp):
+        """After both gathers were summed: the batch (and its pulse) on the scratch engine, then the
+        owned post-batch objects applied here. Returns the batch's reply bytes."""
+        import torch
+
+        from .state_machine import to_host
+
+        G, C = self.shard_count, self.batch_max + 1
+        lay = _gx_layout(n, G, C)
+        g = self.gx
+
+        def recs(off, count):
+            return g[off: off + count * 128].view(count, 128)
+
+        xfer = int(operation) == int(Operation.create_transfers)
+        accs = [recs(lay["ra"], 2 * n), recs(lay["rq"], 2 * G * C)]
+        if xfer:
+            accs.append(recs(lay["rp"], 2 * n))
+        acc = _unique_by_timestamp(torch.cat(accs))[0]
+        xs = [recs(lay["rx"], 2 * n), recs(lay["rd"], G * C), recs(lay["rn"], G)]
+        st = [g[lay["rs"]: lay["rs"] + 2 * n], torch.ones(G * C + G, dtype=torch.uint8, device=g.device)]
+        x, xst = _unique_by_timestamp(torch.cat(xs), torch.cat(st))
+        pn = self.pulse_next()
+        sc = self.scratch
+        sc.reset()
+        L = _lib.lib()
+        _lib.check(L.tbg_open_device(sc.h, acc.data_ptr(), acc.shape[0], x.data_ptr(), xst.data_ptr(), x.shape[0], pn),
+                   "open_device")
+        sc.prepare_timestamp = timestamp
+        sc.commit_window(operation, d_events, [n], [timestamp], self.gx_res.data_ptr(), self.gx_base.data_ptr(),
+                         True, timestamp)
+        sc.sync()
+        base = to_host(self.gx_base)
+        reply = to_host(self.gx_res[: int(base[1]) * 8]).tobytes()
+        pa, na, px, ps, nx, pn2 = (ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_void_p(),
+                                   ctypes.c_uint64(), ctypes.c_uint64())
+        _lib.check(L.tbg_device_state(sc.h, ctypes.byref(pa), ctypes.byref(na), ctypes.byref(px), ctypes.byref(ps),
+                                      ctypes.byref(nx), ctypes.byref(pn2)), "device_state")
+        _lib.check(L.tbg_shard_apply(self.sm.h, pa, na.value, px, ps, nx.value, pn2.value), "shard_apply")
+        self.sm.sync()
+        return reply
+
+
+def _gx_layout(E, G, C):
+    """Byte offsets of the gather buffer (mirror of gx_view, csrc/shard_gx.inc)."""
+    def al(x):
+        return (x + 255) & ~255
+
+    o = 256
+    lay = {}
+    lay["ra"], o = o, al(o + 2 * E * 128)
+    lay["rx"], o = o, al(o + 2 * E * 128)
+    lay["rs"], o = o, al(o + 2 * E)
+    lay["rd"], o = o, al(o + G * C * 128)
+    lay["rn"], o = o, al(o + G * 128)
+    lay["p2"] = o
+    lay["rp"], o = o, al(o + 2 * E * 128)
+    lay["rq"], o = o, al(o + 2 * G * C * 128)
+    lay["bytes"] = o
+    return lay
+
+
+def _unique_by_timestamp(recs, status=None):
+    """Gathered 128-byte records (timestamp at byte 120; 0 = empty slot) -> distinct ones in
+    timestamp order (= creation order, what tbg_open_device expects), with their status bytes."""
+    import torch
+
+    ts = recs.view(torch.int64)[:, 15]
+    keep = ts != 0
+    recs, ts = recs[keep], ts[keep]
+    if status is not None:
+        status = status[keep]
+    order = torch.argsort(ts, stable=True)
+    recs, ts = recs[order], ts[order]
+    if status is not None:
+        status = status[order]
+    first = torch.ones_like(ts, dtype=torch.bool)
+    if ts.numel() > 1:
+        first[1:] = ts[1:] != ts[:-1]
+    recs = recs[first].contiguous()
+    if status is not None:
+        status = status[first].contiguous()
+    return recs, status
+
+
+def commit_general_batch(shards, summed, operation, d_events, n, timestamp):
+    """One batch through the general path on `shards` (all shards in-process, or this process's
+    one); `summed(list of tensors)` sums them across all shards in place. Returns the reply."""
+    summed([s.gather(operation, d_events, n, timestamp, 1) for s in shards])
+    summed([s.gather(operation, d_events, n, timestamp, 2) for s in shards])
+    replies = [s.decide_apply(operation, d_events, n, timestamp) for s in shards]
+    assert all(r == replies[0] for r in replies)
+    return replies[0]
