@@ -250,3 +250,52 @@ def test_pulse_windows_cover_resets_and_rejections():
         mid += m
         rej += r
     assert mid > 0 and rej > 0, (mid, rej)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_due", [3, 4, 5, 8])
+def test_pulse_exactly_cap_due(n_due):
+    """batch_max = 4 and 3, 4, 5 or 8 pending transfers due at one pulse. The scan's buffer-full
+    check precedes each next() (lsm/scan_lookup.zig:151-156): with exactly 4 due the buffer fills
+    before the scan sees the next entry, so the pulse ends buffer_finished, pulse_next_timestamp is
+    the last expired one's expires_at (state_machine.zig:2112-2145) and another pulse follows."""
+    from tigerbeetle_amd import StateMachine
+    from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE, set_u128
+
+    bm = 4
+    gpu = StateMachine(batch_max=bm, accounts_max=64, transfers_max=1024)
+    ref = OracleStateMachine(batch_max=bm)
+    try:
+        ls = Lockstep(gpu, ref)
+        a = np.zeros(2, ACCOUNT_DTYPE)
+        for k in range(2):
+            set_u128(a[k], "id", k + 1)
+            a[k]["ledger"], a[k]["code"] = 1, 1
+        run_protocol(ls, Operation.create_accounts, a, 0)
+        ids = iter(range(100, 1000))
+
+        def xfers(n, timeout, pending=True):
+            t = np.zeros(n, TRANSFER_DTYPE)
+            for k in range(n):
+                set_u128(t[k], "id", next(ids))
+                set_u128(t[k], "debit_account_id", 1)
+                set_u128(t[k], "credit_account_id", 2)
+                set_u128(t[k], "amount", 10)
+                t[k]["ledger"], t[k]["code"] = 1, 1
+                t[k]["flags"] = 2 if pending else 0
+                t[k]["timeout"] = timeout
+            return t
+
+        left = n_due
+        while left:
+            run_protocol(ls, Operation.create_transfers, xfers(min(bm, left), 1), 0)
+            left -= min(bm, left)
+        run_protocol(ls, Operation.create_transfers, xfers(1, 30), 0)  # a later live entry
+        for k in range(4):  # past the timeouts, then a few batches: one or more pulses
+            run_protocol(ls, Operation.create_transfers, xfers(1, 0, pending=False), 2 * NS_PER_S if k == 0 else 0)
+        assert ls.pulses >= 2
+        _compare_final(gpu, ref)
+        assert (ref.dump_transfer_status() == 4).sum() == n_due
+    finally:
+        gpu.close()
+        ref.close()

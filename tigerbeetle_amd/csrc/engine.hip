@@ -1258,7 +1258,9 @@ __global__ void __launch_bounds__(1024) k_pulse(Dev d, Scratch s, uint64_t T, ui
   if (!last_block_done(&g->pulse_done, &flag)) return;
   // ---- the last block: selection, finish, window check, apply ----
   const uint32_t m = __hip_atomic_load(&g->cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const bool select_all = m <= cap;
+  // the buffer-full check precedes each next() (lsm/scan_lookup.zig:151-156): with exactly `cap`
+  // entries due the scan ends buffer_finished too, and pulse_next is the last one's expires_at
+  const bool select_all = m < cap;
   if (threadIdx.x == 0) {
     prefix_hi = 0;
     prefix_lo = 0;

@@ -55,7 +55,8 @@ __global__ void k_xwin_decide(Dev d, Scratch s, WinDesc w, uint32_t cap) {
   if (WIN_REJECTED(g)) return;
   // (history rows hold the balances after each event: an expiry inside the window would move them)
   bool bad = g->hot_count != 0 || g->batch_huge || ovf128(g->ovf_bound, g->batch_amount_sum) || (g->win_flags & 16u);
-  for (uint32_t b = 1; b < w.nb; b++) bad = bad || s.xw_cnt[b] > cap;
+  // (a pulse that fills its buffer, cap entries or more, ends buffer_finished: not modelled)
+  for (uint32_t b = 1; b < w.nb; b++) bad = bad || s.xw_cnt[b] >= cap;
   if (!bad) return;
   atomicOr(&g->window_error, 1u);
   g->hot_count = 0;

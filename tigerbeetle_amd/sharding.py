@@ -223,6 +223,7 @@ class ShardedStateMachine:
         x, xst = _unique_by_timestamp(torch.cat(xs), torch.cat(st))
         pn = self.pulse_next()
         sc = self.scratch
+        torch.cuda.synchronize(self.device)  # the dedupe ran on torch's stream; the open reads it on the scratch's
         sc.reset()
         L = _lib.lib()
         _lib.check(L.tbg_open_device(sc.h, acc.data_ptr(), acc.shape[0], x.data_ptr(), xst.data_ptr(), x.shape[0], pn),
