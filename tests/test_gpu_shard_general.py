@@ -167,3 +167,55 @@ def test_shard_general_two_rank_gloo(tmp_path):
         assert st[o].tobytes() == ref.dump_transfer_status().tobytes()
     finally:
         ref.close()
+
+
+def _general_stream(sh, ref, op, batches, ticks):
+    for ev, tick in zip(batches, ticks):
+        g, _ = sh.commit_any(op, [ev], tick)
+        assert g == [run_protocol(ref, op, ev, tick)]
+        assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_shard_cfg3_shape(G):
+    """cfg3's shape (Zipf(1.2) debits over accounts with debits_must_not_exceed_credits, funded from
+    treasury accounts) on G shards: every transfer batch reads balances across shards."""
+    bm, n_acc, top, treasury = 512, 3000, 100, 50
+    sh = LocalShards(G, bm, 4096, 1 << 15, bm)
+    ref = OracleStateMachine(batch_max=bm)
+    try:
+        acc = workload.accounts_cfg3(0, n_acc + treasury, 45, n_acc, top)
+        _general_stream(sh, ref, Operation.create_accounts, [acc[i:i + bm] for i in range(0, len(acc), bm)],
+                        [0] * ((len(acc) + bm - 1) // bm))
+        fund = workload.funding_cfg3(0, n_acc, 45, n_acc, treasury, 20_000, 10**15)
+        _general_stream(sh, ref, Operation.create_transfers, [fund[i:i + bm] for i in range(0, len(fund), bm)],
+                        [0] * ((len(fund) + bm - 1) // bm))
+        xf = workload.transfers_zipf(0, 6 * bm, 45, n_acc, workload.zipf_cdf(n_acc))
+        _general_stream(sh, ref, Operation.create_transfers, [xf[i:i + bm] for i in range(0, len(xf), bm)], [0] * 6)
+        _check(sh, ref)
+    finally:
+        sh.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_shard_cfg4_shape(G):
+    """cfg4's shape (30 % pending with 1-60 s timeouts, posts / voids of earlier pending transfers,
+    chains with injected failures), +1 s per batch so a pulse with expiries precedes most batches."""
+    bm, n_acc = 512, 2000
+    sh = LocalShards(G, bm, 4096, 1 << 15, bm)
+    ref = OracleStateMachine(batch_max=bm)
+    try:
+        acc = workload.accounts(0, n_acc, seed=46)
+        _general_stream(sh, ref, Operation.create_accounts, [acc[i:i + bm] for i in range(0, n_acc, bm)],
+                        [0] * ((n_acc + bm - 1) // bm))
+        xf = workload.transfers_cfg4(0, 40 * bm, 46, n_acc, bm)
+        _general_stream(sh, ref, Operation.create_transfers, [xf[i:i + bm] for i in range(0, len(xf), bm)],
+                        [NS_PER_S] * 40)
+        _check(sh, ref)
+        assert (ref.dump_transfer_status() == 4).sum() > 0  # expiries ran on the shards
+    finally:
+        sh.close()
+        ref.close()
