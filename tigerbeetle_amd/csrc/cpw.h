@@ -77,8 +77,11 @@ __global__ void __launch_bounds__(256) k_cc_keys(Dev d, Scratch s, uint32_t E) {
 }
 
 // Component starts in the sorted order.
-// (one counter atomic per wave: ~140K component starts per cfg4 window would serialize on it)
-__global__ void __launch_bounds__(256) k_cc_segs(Dev d, Scratch s, uint32_t E) {
+// One counter atomic per 1024-thread block: same-address atomics serialize at the memory side
+// (~140K component starts in a cfg4 window; even one per wave cost ~90 us).
+__global__ void __launch_bounds__(1024) k_cc_segs(Dev d, Scratch s, uint32_t E) {
+  __shared__ uint32_t lds[1024 / 64];
+  __shared__ uint32_t base;
   if (!cpw_active(d.g)) return;
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   bool start = false;
@@ -86,14 +89,12 @@ __global__ void __launch_bounds__(256) k_cc_segs(Dev d, Scratch s, uint32_t E) {
     const uint32_t key = s.rkey[k];
     start = key != RES_DUMMY && (k == 0 || s.rkey[k - 1] != key);
   }
-  const unsigned long long m = __ballot(start);
-  if (!m) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __builtin_ctzll(m);
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(&d.g->cc_count, (uint32_t)__popcll(m));
-  base = __shfl(base, leader, 64);
-  if (start) s.cc_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = k;
+  uint32_t tot;
+  const uint32_t r = block_excl<1024 / 64>(start ? 1u : 0u, lds, &tot);
+  if (tot == 0) return;
+  if (threadIdx.x == 0) base = atomicAdd(&d.g->cc_count, tot);
+  __syncthreads();
+  if (start) s.cc_list[base + r] = k;
 }
 
 // One walker per component: events rval[start .. start + len), undo records from 5 * start.
@@ -112,7 +113,10 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
     while (start + len < w.E && s.rkey[start + len] == key) len++;
   }
   // statistics (tbg_debug_counters): [5] longest component, [6] components, [7] W events walked;
-  // one lane per wave adds (same-address atomics from every component serialize at the memory side)
+  // one lane per block adds (same-address atomics from every wave serialize at the memory side)
+  __shared__ uint32_t st_mx, st_n, st_sum;
+  if (threadIdx.x == 0) st_mx = st_n = st_sum = 0;
+  __syncthreads();
   uint32_t mx = len, sum = len;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -122,9 +126,15 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
   }
   const uint32_t n_on = (uint32_t)__popcll(__ballot(on));
   if ((threadIdx.x & 63) == 0 && n_on) {
-    atomicMax((unsigned long long*)&g->dbg[5], (unsigned long long)mx);
-    atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)n_on);
-    atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)sum);
+    atomicMax(&st_mx, mx);
+    atomicAdd(&st_n, n_on);
+    atomicAdd(&st_sum, sum);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && st_n) {
+    atomicMax((unsigned long long*)&g->dbg[5], (unsigned long long)st_mx);
+    atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)st_n);
+    atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)st_sum);
   }
   if (!on) return;
   Walker wk;

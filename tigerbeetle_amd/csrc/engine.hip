@@ -572,7 +572,9 @@ __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, u
     const u128 sum = d.g->ovf_bound + d.g->batch_amount_sum;
     if (ovf_mode || (sum >> 126) != 0) bad = true;
   }
-  if (XFER && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(&d.g->res_inelig, 1u);
+  // a sticky flag: read before the atomic (same-address atomics from every wave serialize)
+  if (XFER && __any(bad) && (threadIdx.x & 63) == 0 && !__hip_atomic_load(&d.g->res_inelig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicOr(&d.g->res_inelig, 1u);
 }
 
 #include "cpw.h"
@@ -1021,6 +1023,9 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   wave_sync();
   // this event's output record (the input record, stamped; W events carry theirs in s.t2)
   uint4 rec[8];
+  // its live expires_at entry, if any (appended per wave below: one counter atomic per wave)
+  bool xapp = false;
+  ExpEntry xent;
   if (XFER && (cls & C_W)) {
     const uint4* t2 = reinterpret_cast<const uint4*>(&s.t2[i]);
 #pragma unroll
@@ -1109,12 +1114,10 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
             // (pulse_next is k_pn's: it also counts creations that a failing chain rolled back)
             const bool visible = !(ts >> 63) && expires_at <= TB_TIMESTAMP_MAX;
             if (st == TB_PENDING_PENDING && visible) {
-              const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), 1ull);
-              ExpEntry e;
-              e.expires_at = expires_at;
-              e.slot = (uint32_t)slot;
-              e.pad = 0;
-              d.exp[*d.exp_cur][q] = e;
+              xapp = true;
+              xent.expires_at = expires_at;
+              xent.slot = (uint32_t)slot;
+              xent.pad = 0;
             }
           }
         }
@@ -1132,6 +1135,17 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
       acc_insert(d.acc_tab, d.acc_mask, rw_u128(rec[0]), (uint32_t)slot, rec[7].x, aflags);
       if (aflags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS | TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS))
         atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->limited_accounts), 1ull);
+    }
+  }
+  if (XFER) {
+    const unsigned long long m = __ballot(xapp);
+    if (m) {
+      const int leader = __builtin_ctzll(m);
+      unsigned long long q = 0;
+      if ((int)lane == leader)
+        q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), (unsigned long long)__popcll(m));
+      q = __shfl(q, leader, 64);
+      if (xapp) d.exp[*d.exp_cur][q + (unsigned long long)__popcll(m & ((1ull << lane) - 1))] = xent;
     }
   }
   // Compact this wave's inserted records in LDS, then store them as one contiguous run (a wave
@@ -1243,18 +1257,31 @@ __global__ void __launch_bounds__(1024) k_pulse(Dev d, Scratch s, uint64_t T, ui
   const ExpEntry* list = d.exp[cur];
   ExpEntry* alt = d.exp[cur ^ 1];
   const uint64_t count = g->exp_count;
+  // (appends aggregated per wave, the minimum per wave: same-address atomics serialize)
+  const uint32_t lane = threadIdx.x & 63;
+  const unsigned long long lt = (1ull << lane) - 1;
+  unsigned long long nmin = ~0ull;
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < count; j += (uint64_t)gridDim.x * blockDim.x) {
     const ExpEntry e = list[j];
-    if (d.xstatus[e.slot] != TB_PENDING_PENDING) continue;  // removed from the index
-    if (e.expires_at <= T) {
-      const uint32_t k = atomicAdd(&g->cand_count, 1u);
-      s.cand[k] = e;
-    } else {
-      const uint32_t k = atomicAdd(&g->alt_count, 1u);
-      alt[k] = e;
-      atomicMin(reinterpret_cast<unsigned long long*>(&g->next_min), (unsigned long long)e.expires_at);
+    const bool live = d.xstatus[e.slot] == TB_PENDING_PENDING;  // else removed from the index
+    const bool due = live && e.expires_at <= T;
+    const bool later = live && !due;
+    const unsigned long long md = __ballot(due), ml = __ballot(later);
+    const int ld = md ? __builtin_ctzll(md) : 0, ll = ml ? __builtin_ctzll(ml) : 0;
+    uint32_t bd = 0, bl = 0;
+    if (md && (int)lane == ld) bd = atomicAdd(&g->cand_count, (uint32_t)__popcll(md));
+    if (ml && (int)lane == ll) bl = atomicAdd(&g->alt_count, (uint32_t)__popcll(ml));
+    bd = __shfl(bd, ld, 64);
+    bl = __shfl(bl, ll, 64);
+    if (due) s.cand[bd + (uint32_t)__popcll(md & lt)] = e;
+    if (later) {
+      alt[bl + (uint32_t)__popcll(ml & lt)] = e;
+      nmin = umin64(nmin, e.expires_at);
     }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nmin = umin64(nmin, (unsigned long long)__shfl_xor(nmin, o, 64));
+  if (lane == 0 && nmin != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(&g->next_min), nmin);
   if (!last_block_done(&g->pulse_done, &flag)) return;
   // ---- the last block: selection, finish, window check, apply ----
   const uint32_t m = __hip_atomic_load(&g->cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

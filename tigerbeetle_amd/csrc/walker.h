@@ -299,7 +299,8 @@ struct Walker {
       s.cls[i] |= C_PNOP;
       // may reset pulse_next (needs expires_at <= pulse_next as it was after the window's pulse,
       // which holds until k_final): k_final then replays the window's ops in order
-      if (s.pnv[i] <= d.g->pulse_next) atomicOr(&d.g->win_flags, 8u);
+      if (s.pnv[i] <= d.g->pulse_next && !(__hip_atomic_load(&d.g->win_flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8u))
+        atomicOr(&d.g->win_flags, 8u);
     }
     const uint8_t st = (t.flags & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
     if (pc >= 0) {
