@@ -34,6 +34,10 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 
+// Onesweep radix sort at every size (merge_sort_limit 0): rocprim's default picks its merge-sort
+// path up to 2^20 items, ~11 launches (~140 us) for a 1M-event window's keys.
+using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+
 #include "../../include/tbg.h"
 #include "dev_common.h"
 #include "sm_logic.h"

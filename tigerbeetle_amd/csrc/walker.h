@@ -79,6 +79,7 @@ __device__ inline void bmap_set_committed(BEntry* bm, uint32_t e, uint32_t epoch
 // walker for a later event), loaded one event ahead so the walk pays only its dynamic reads.
 struct WPre {
   uint32_t i, cls, b, code, id_tslot, id_ent, dr, cr, p_tslot, pid_ent;
+  bool id_alone;  // no other event of the window carries this id: no earlier commit of it to look up
 };
 
 struct Walker {
@@ -204,6 +205,8 @@ struct Walker {
       e.p_tslot = s.p_tslot[i];
       e.pid_ent = s.pid_ent[i];
     }
+    // the id's claim count is final once k_ct_prep / k_claim_fix ran (only its commit field changes)
+    e.id_alone = (e.cls & C_REACH) && e.id_ent != NONE32 && bmap_idc(s.bmap, e.id_ent, epoch) == 1;
     return e;
   }
 
@@ -215,7 +218,7 @@ struct Walker {
     t.timestamp = win_ts(*w, e.b, i);
     if (e.cls & C_POSTVOID) return post_or_void(e, t);
     if (e.id_tslot != NONE32) return ct_exists(t, d.xr[e.id_tslot]);
-    const int32_t c = bmap_committed(s.bmap, e.id_ent, epoch);
+    const int32_t c = e.id_alone ? -1 : bmap_committed(s.bmap, e.id_ent, epoch);
     if (c >= 0) return ct_exists(t, s.t2[c]);
     const uint32_t drs = e.dr, crs = e.cr;
     tb_account_t* dra = &d.acc[drs];
@@ -283,7 +286,7 @@ struct Walker {
     uint32_t r = pv_against(t, p, &amount);
     if (r != CONT) return r;
     if (e.id_tslot != NONE32) return pv_exists(t, d.xr[e.id_tslot], p);
-    const int32_t c = bmap_committed(s.bmap, e.id_ent, epoch);
+    const int32_t c = e.id_alone ? -1 : bmap_committed(s.bmap, e.id_ent, epoch);
     if (c >= 0) return pv_exists(t, s.t2[c], p);
     uint8_t pst = pc >= 0 ? s.bstatus[pc] : d.xstatus[pslot];
     if (pst == TB_PENDING_PENDING && xw_expired_before(*w, p, s.batch[i])) pst = TB_PENDING_EXPIRED;
