@@ -137,7 +137,11 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
     atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)st_sum);
   }
   if (!on) return;
+  __shared__ uint2 pcache[256 * WCACHE];
+  uint2* mine = pcache + threadIdx.x * WCACHE;
+  for (int k = 0; k < WCACHE; k++) mine[k] = make_uint2(NONE32, 0);
   Walker wk;
+  wk.pcache = mine;
   wk.d = d;
   wk.s = s;
   wk.s.undo = s.undo + 5ull * start;

@@ -176,6 +176,8 @@ enum : uint32_t {
   C_HIST = 1u << 21,       // touches an account with flags.history: its history row needs the balances
                            // after it in order, so it runs on the sequential walker
   C_PREP_REC = 1u << 22,   // k_ct_prep stored the stamped record at slot base + i (k_final keeps it if final)
+  C_IDALONE = 1u << 23,    // W, transfers: no other event of the window carries this id (k_classify; the
+                           // walker skips looking up an earlier commit of it)
 };
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

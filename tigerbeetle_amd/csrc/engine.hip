@@ -509,6 +509,13 @@ __device__ inline bool res_bad(const Scratch& s, uint32_t j, uint32_t cls, uint3
   return bmap_idc(s.bmap, e, epoch) > 1 || bmap_pidc(s.bmap, e, epoch) > 0;
 }
 
+// The walker's id fact for a W transfer event: claim-free windows give every id a private entry.
+template <bool XFER>
+__device__ inline uint32_t id_alone_bit(const Scratch& s, uint32_t j, uint32_t cls, uint32_t epoch, bool claim_free) {
+  if (!XFER || !(cls & C_REACH)) return 0u;
+  return (claim_free || bmap_idc(s.bmap, s.id_ent[j], epoch) == 1) ? C_IDALONE : 0u;
+}
+
 template <bool XFER>
 __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinDesc& w, uint32_t i, uint32_t epoch,
                                       bool ovf_mode, bool claim_free, bool any_hot) {
@@ -520,7 +527,7 @@ __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinD
   if (!linked) {
     // singleton (:1255-1259, :1289-1290)
     if (is_w<XFER>(d, s, i, &cls, epoch, ovf_mode, claim_free, any_hot)) {
-      s.cls[i] = cls | C_W;
+      s.cls[i] = cls | C_W | id_alone_bit<XFER>(s, i, cls, epoch, claim_free);
       return res_bad(s, i, cls, epoch);
     }
     const uint32_t code = s.code[i];
@@ -543,7 +550,7 @@ __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinD
   for (uint32_t j = i; j <= end; j++) {
     const uint32_t cj = s.cls[j];
     if (any_w) {
-      s.cls[j] = cj | C_W;
+      s.cls[j] = cj | C_W | id_alone_bit<XFER>(s, j, cj, epoch, claim_free);
       continue;
     }
     uint32_t code = s.code[j];

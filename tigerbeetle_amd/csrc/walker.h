@@ -99,6 +99,16 @@ struct Walker {
   // balance delta is a no-return 64-bit add on the low word (mod 2^64; the true value never leaves
   // the low word) and no walker waits for an atomic's result.
   bool small_bal = false;
+  // This walker's recent commits (id key-map entry -> event index), direct-mapped in LDS: a
+  // post/void of a pending transfer its component created finds it without the key-map read (a
+  // component's keys are committed by its own walker only; cleared on every rollback). nullptr: off.
+  uint2* pcache = nullptr;
+#define WCACHE 8
+  __device__ __attribute__((always_inline)) int32_t pcache_find(uint32_t ent) const {
+    if (!pcache) return -1;
+    const uint2 c = pcache[ent & (WCACHE - 1)];
+    return c.x == ent ? (int32_t)c.y : -1;
+  }
 
   __device__ __attribute__((always_inline)) void log_bal(uint32_t slot) {
     if (!scope) return;
@@ -134,6 +144,8 @@ struct Walker {
     r.old[0] = v;
   }
   __device__ __attribute__((always_inline)) void rollback() {
+    if (pcache)
+      for (int k = 0; k < WCACHE; k++) pcache[k] = make_uint2(NONE32, 0);
     while (undo_n) {
       const UndoRec& r = s.undo[--undo_n];
       switch (r.kind) {
@@ -186,8 +198,11 @@ struct Walker {
     log_small(UNDO_INS, i, 0);
     s.ins[i] = 1;
     const uint32_t e = s.id_ent[i];
-    log_small(UNDO_COMMIT, e, s.bmap[e].commit);
+    // (the entry had no commit this window, or the caller would have found it: undo restores
+    // "none", epoch 0, without reading the old word)
+    log_small(UNDO_COMMIT, e, 0);
     bmap_set_committed(s.bmap, e, epoch, (int32_t)i);
+    if (pcache) pcache[e & (WCACHE - 1)] = make_uint2(e, i);
   }
 
   template <bool XFER>
@@ -205,8 +220,7 @@ struct Walker {
       e.p_tslot = s.p_tslot[i];
       e.pid_ent = s.pid_ent[i];
     }
-    // the id's claim count is final once k_ct_prep / k_claim_fix ran (only its commit field changes)
-    e.id_alone = (e.cls & C_REACH) && e.id_ent != NONE32 && bmap_idc(s.bmap, e.id_ent, epoch) == 1;
+    e.id_alone = (e.cls & C_IDALONE) != 0;  // k_classify
     return e;
   }
 
@@ -275,7 +289,8 @@ struct Walker {
       drs = e.dr;
       crs = e.cr;
     } else {
-      pc = bmap_committed(s.bmap, e.pid_ent, epoch);
+      pc = pcache_find(e.pid_ent);
+      if (pc < 0) pc = bmap_committed(s.bmap, e.pid_ent, epoch);
       if (pc < 0) return TB_CT_PENDING_TRANSFER_NOT_FOUND;
       pp = &s.t2[pc];
       drs = s.dr_slot[pc];
@@ -288,7 +303,8 @@ struct Walker {
     if (e.id_tslot != NONE32) return pv_exists(t, d.xr[e.id_tslot], p);
     const int32_t c = e.id_alone ? -1 : bmap_committed(s.bmap, e.id_ent, epoch);
     if (c >= 0) return pv_exists(t, s.t2[c], p);
-    uint8_t pst = pc >= 0 ? s.bstatus[pc] : d.xstatus[pslot];
+    const uint8_t pst0 = pc >= 0 ? s.bstatus[pc] : d.xstatus[pslot];
+    uint8_t pst = pst0;
     if (pst == TB_PENDING_PENDING && xw_expired_before(*w, p, s.batch[i])) pst = TB_PENDING_EXPIRED;
     r = pv_status(pst);
     if (r != CONT) return r;
@@ -307,10 +323,10 @@ struct Walker {
     }
     const uint8_t st = (t.flags & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
     if (pc >= 0) {
-      log_small(UNDO_BST, (uint32_t)pc, s.bstatus[pc]);
+      log_small(UNDO_BST, (uint32_t)pc, pst0);
       s.bstatus[pc] = st;
     } else {
-      log_small(UNDO_XST, pslot, d.xstatus[pslot]);
+      log_small(UNDO_XST, pslot, pst0);
       d.xstatus[pslot] = st;
     }
     const u128 pa = U(p.amount);
@@ -350,7 +366,7 @@ struct Walker {
     if (c >= 0) return ca_exists(evs[i], evs[c]);
     log_small(UNDO_INS, i, 0);
     s.ins[i] = 1;
-    log_small(UNDO_COMMIT, e, s.bmap[e].commit);
+    log_small(UNDO_COMMIT, e, 0);  // no commit of this id this window (c < 0 above)
     bmap_set_committed(s.bmap, e, epoch, (int32_t)i);
     return TB_CA_OK;
   }
