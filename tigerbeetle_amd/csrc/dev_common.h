@@ -110,7 +110,7 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t cpw_done;    // the component walkers decided every W event
   uint64_t cpw_events_total;  // cumulative W events decided by component walkers
   uint32_t small_win;   // this window: ovf_bound + window amounts < 2^64 (set by k_walk; k_final reads it)
-  uint32_t pad3;
+  uint32_t cold_count;  // hot ranks found non-binding this window (k_bind_decide; k_bind_finish resets)
   // Sorted transfer prefix: records [0, x_sorted) have ids < 2^64, strictly increasing with the
   // slot, and are not in the hash table (found by binary search, x_prefix_find). A window whose
   // ids are strictly increasing and above every stored id extends it instead of hashing its inserts

@@ -100,7 +100,7 @@ __device__ inline uint32_t acc_probe_from(const AccEntry* __restrict__ tab, uint
 // A balance-reading decision makes the read account hot for this window: every event touching it
 // is then decided in order (resolver.h or the walker). The first marker assigns the account its
 // dense rank (one counter atomic per wave).
-__device__ inline void mark_hot(Dev d, uint32_t slot, uint32_t epoch) {
+__device__ inline void mark_hot(Dev d, Scratch s, uint32_t slot, uint32_t epoch) {
   // a plain read first: a hot account is marked by many events (a stale read only costs the atomic)
   bool first = false;
   if (d.hot[slot] != epoch) first = atomicExch(&d.hot[slot], epoch) != epoch;
@@ -111,7 +111,101 @@ __device__ inline void mark_hot(Dev d, uint32_t slot, uint32_t epoch) {
   uint32_t base = 0;
   if (lane == leader) base = atomicAdd(&d.g->hot_count, (uint32_t)__popcll(m));
   base = __shfl(base, leader, 64);
-  d.hot_rank[slot] = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+  const uint32_t rank = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+  d.hot_rank[slot] = rank;
+  s.bind_slot[rank] = slot;
+  s.bind_adv[rank] = 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Non-binding limits. A limit check reads an account's balances (debits_must_not_exceed_credits:
+// dp + dpo + amount > cpo, tigerbeetle.zig:31-39); within a window only the window's own debits can
+// raise dp + dpo (posts and voids of pending transfers and expiries lower it, credits raise cpo).
+// So if the account's balances at the window start plus EVERY debit amount of the window that
+// reaches its check still pass (dp + dpo + sum <= cpo), every one of those checks passes whatever
+// the order and the other outcomes: the account needs no ordering. The same for credits of a
+// credits_must_not_exceed_debits account. Balancing transfers read the balances for their amount:
+// their accounts stay hot. k_bind_sum folds the sums per hot rank (LDS hash per block, one global
+// add per distinct rank per block: Zipf-hot accounts would serialize on one address otherwise),
+// k_bind_decide un-marks the non-binding accounts, k_classify then drops their read bits.
+// ------------------------------------------------------------------------------------------------
+#define BIND_LDS 1024
+#define BIND_FORCE (1ull << 63)
+#define BIND_AMOUNT_MAX (1ull << 40)  // larger amounts keep their account hot (the sums stay < 2^63)
+
+__device__ inline void bind_add(Dev d, Scratch s, uint32_t* tk, unsigned long long* tv, uint32_t slot, u128 amount,
+                                bool force) {
+  const uint32_t r = d.hot_rank[slot];
+  if (force || amount >= BIND_AMOUNT_MAX) {
+    atomicOr(&s.bind_adv[r], BIND_FORCE);
+    return;
+  }
+  const unsigned long long v = (unsigned long long)amount;
+  uint32_t h = (r * 2654435761u) & (BIND_LDS - 1);
+  for (int probe = 0; probe < 8; probe++, h = (h + 1) & (BIND_LDS - 1)) {
+    uint32_t k = tk[h];
+    if (k == NONE32) k = atomicCAS(&tk[h], NONE32, r), k = (k == NONE32) ? r : k;
+    if (k == r) {
+      atomicAdd(&tv[h], v);
+      return;
+    }
+  }
+  atomicAdd(&s.bind_adv[r], v);  // LDS table crowded: straight to memory
+}
+
+__global__ void __launch_bounds__(256) k_bind_sum(Dev d, Scratch s, uint32_t E, uint32_t epoch) {
+  __shared__ uint32_t tk[BIND_LDS];
+  __shared__ unsigned long long tv[BIND_LDS];
+  if (WIN_REJECTED(d.g) || !d.g->hot_count) return;
+  for (uint32_t j = threadIdx.x; j < BIND_LDS; j += blockDim.x) {
+    tk[j] = NONE32;
+    tv[j] = 0;
+  }
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < E) {
+    const uint32_t cls = s.cls[i];
+    const bool bal = cls & C_BAL;
+    if (cls & C_READS_DR) bind_add(d, s, tk, tv, s.dr_slot[i], s.amt[i], bal);
+    if (cls & C_READS_CR) bind_add(d, s, tk, tv, s.cr_slot[i], s.amt[i], bal);
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < BIND_LDS; j += blockDim.x)
+    if (tk[j] != NONE32) atomicAdd(&s.bind_adv[tk[j]], tv[j]);
+}
+
+// Per hot rank: un-mark the account when its checks cannot fail this window.
+__global__ void __launch_bounds__(256) k_bind_decide(Dev d, Scratch s) {
+  Globals* g = d.g;
+  if (WIN_REJECTED(g)) return;
+  const uint32_t n = g->hot_count;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  bool cold = false;
+  if (r < n) {
+    const unsigned long long adv = s.bind_adv[r];
+    if (!(adv & BIND_FORCE)) {
+      const uint32_t slot = s.bind_slot[r];
+      const tb_account_t& a = d.acc[slot];
+      const u128 sum_d = U(a.debits_pending) + U(a.debits_posted), sum_c = U(a.credits_pending) + U(a.credits_posted);
+      if (a.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) {
+        const u128 x = sum_d + (u128)adv;
+        cold = sum_d >= U(a.debits_pending) && x >= sum_d && x <= U(a.credits_posted);
+      } else if (a.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) {
+        const u128 x = sum_c + (u128)adv;
+        cold = sum_c >= U(a.credits_pending) && x >= sum_c && x <= U(a.debits_posted);
+      }
+      if (cold) d.hot[slot] = 0;
+    }
+  }
+  const unsigned long long m = __ballot(cold);
+  if (m && (threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(&g->cold_count, (uint32_t)__popcll(m));
+}
+
+// Every hot account non-binding: the window reads no balance after all (cpw / order-free paths).
+__global__ void k_bind_finish(Globals* g) {
+  if (WIN_REJECTED(g)) return;
+  if (g->hot_count && g->cold_count == g->hot_count) g->hot_count = 0;
+  g->cold_count = 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -299,8 +393,8 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     if (cls & C_REACH) atomicMax(&id_max, (unsigned long long)x_id_key(t.id));
     prec = (cls & C_PREP_REC) != 0;
     // Hot marks: the first marker of an account this window gives it the next dense rank.
-    if (cls & C_READS_DR) mark_hot(d, dr_slot, epoch);
-    if (cls & C_READS_CR) mark_hot(d, cr_slot, epoch);
+    if (cls & C_READS_DR) mark_hot(d, s, dr_slot, epoch);
+    if (cls & C_READS_CR) mark_hot(d, s, cr_slot, epoch);
     s.code[i] = code;
     s.cls[i] = cls;
     s.batch[i] = (uint16_t)b;
@@ -492,6 +586,11 @@ __device__ inline bool is_u(const Scratch& s, uint32_t j, uint32_t cls, uint32_t
 template <bool XFER>
 __device__ inline bool is_w(const Dev& d, const Scratch& s, uint32_t j, uint32_t* cls, uint32_t epoch, bool ovf_mode,
                             bool claim_free, bool any_hot) {
+  // a read of a non-binding account (k_bind_decide un-marked it) passes whatever the order
+  if (XFER && (*cls & (C_READS_DR | C_READS_CR)) && !(*cls & C_BAL)) {
+    if ((*cls & C_READS_DR) && d.hot[s.dr_slot[j]] != epoch) *cls &= ~C_READS_DR;
+    if ((*cls & C_READS_CR) && d.hot[s.cr_slot[j]] != epoch) *cls &= ~C_READS_CR;
+  }
   if (is_u<XFER>(s, j, *cls, epoch, ovf_mode, claim_free)) {
     *cls |= C_U;
     return true;

@@ -105,6 +105,10 @@ struct Scratch {
   uint2* rlink;                               // relax.h: per sorted entry: other side's entry and rank
   uint32_t *heavy, *light;                    // hot ranks by walker kind
   uint32_t *cc_parent, *cc_list;              // component-parallel walker (cpw.h)
+  // non-binding limits (k_bind_*): per hot rank its account slot and the adverse sum of the window
+  // (debits of a debits<=credits account, credits of a credits<=debits one; bit 63 = must stay hot)
+  uint32_t* bind_slot;
+  unsigned long long* bind_adv;
   // pulse_next (k_pn): per event the op's value (C_PNOP) and, for a walker post/void of a pending
   // transfer created in the window, that transfer's event index; per segment the min creation value
   // and the count of resets among the events that ran ok
