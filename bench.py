@@ -128,8 +128,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (commit time)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-phase-timing", action="store_true")
-    p.add_argument("--resolver", default="relax", choices=["relax", "wait", "off"],
-                   help="balance-limit windows: windowed relaxation (default), wait-based walkers, walker only")
+    p.add_argument("--resolver", default="chunks", choices=["chunks", "relax", "wait", "off"],
+                   help="balance-limit windows: chunked single-workgroup resolver where the window fits it "
+                        "(default), grid-wide windowed relaxation, wait-based walkers, walker only")
     p.add_argument("--verify", action="store_true", help="setup all ok; cfg1/cfg2: every transfer ok")
     p.add_argument("--host-fed-transfers", type=int, default=None,
                    help="cfg1/cfg2: after the timed run, commit this many further transfers of the same stream "
@@ -549,7 +550,7 @@ def main():
     sm = StateMachine(device=device, batch_max=BATCH, accounts_max=n_acc_total,
                       transfers_max=n_xfer + n_setup + args.host_fed_transfers,
                       window_events_max=win * BATCH,
-                      resolver={"relax": True, "wait": "wait", "off": False}[args.resolver],
+                      resolver={"chunks": True, "relax": "relax", "wait": "wait", "off": False}[args.resolver],
                       change_log=args.change_log)
     stream = sm.stream
     ext = torch.cuda.ExternalStream(stream)

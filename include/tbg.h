@@ -49,6 +49,9 @@ typedef struct tbg_config {
 /* Reject (TBG_E_WINDOW) every multi-batch window in which a pulse falls due, instead of modelling
    the pulses inside windows that span a second or more (tigerbeetle_amd/csrc/xwin.h). */
 #define TBG_FLAG_NO_XWIN 16u
+/* Resolve balance-limit windows with the grid-wide windowed relaxation (relax.h) even when their
+   hot accounts fit the single-workgroup chunked resolver (chunks.h, the default). Same results. */
+#define TBG_FLAG_NO_CHUNKS 32u
 
 #define TBG_OK 0
 #define TBG_E_INVALID (-1)   /* input_valid() would reject the request */
@@ -299,6 +302,7 @@ typedef struct tbg_stats {
     uint64_t resolver_events; /* of which the account-parallel resolver decided */
     uint64_t component_events; /* of which component-parallel walkers decided */
     uint64_t sorted_transfers; /* leading transfer records in the sorted id prefix (not hashed) */
+    uint64_t chunked_windows;  /* balance-limit windows the chunked resolver decided */
 } tbg_stats;
 int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
 

@@ -156,7 +156,7 @@ def test_geometry_cfg3_zipf_limits():
     from tigerbeetle_amd import StateMachine
 
     seed, top, treasury, fund, fund_id = 45, 1000, 1000, 1_000_000, 10**15
-    n_win, win = 2, 32
+    n_win, win = 4, 32
     n_x = n_win * win * BM
     gpu = StateMachine(batch_max=BM, accounts_max=N_ACC + treasury, transfers_max=n_x + N_ACC,
                        window_events_max=128 * BM)
@@ -180,6 +180,7 @@ def test_geometry_cfg3_zipf_limits():
             fails += sum(len(x) // 8 for x in r)
         assert fails > 0  # exceeds_credits happens
         assert gpu.stats()["resolver_events"] > 0
+        assert gpu.stats()["chunked_windows"] == n_win  # the single-workgroup resolver (chunks.h)
         _check_digest(gpu, ref)
     finally:
         gpu.close()

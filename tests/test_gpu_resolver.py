@@ -89,14 +89,19 @@ def _run(resolver, seed, n_acc, win, bm, n_windows, pending_pct, zipf_s, amount_
     (5, 100, 4, 2048, 20, 1.2, 1 << 61), # window amount sums above 2^62: 128-bit walker steps
 ])
 def test_resolver_matches_oracle_and_walker(seed, n_acc, win, bm, pending_pct, zipf_s, amount_max, monkeypatch):
-    rep_r, st_r = _run(True, seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
-    assert st_r["resolver_events"] > 0
+    rep_r, st_r = _run("relax", seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
+    assert st_r["resolver_events"] > 0 and st_r["chunked_windows"] == 0
+    # the chunked single-workgroup resolver (default) where the window fits it (amounts < 2^62)
+    rep_k, st_k = _run(True, seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
+    assert st_k["resolver_events"] > 0
+    assert (st_k["chunked_windows"] > 0) == (amount_max < 1 << 60)
+    assert rep_r == rep_k
     rep_x, st_x = _run("wait", seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
     assert st_x["resolver_events"] > 0
     assert rep_r == rep_x
     # relaxation windows much smaller than the commit window: many chunk advances
     monkeypatch.setenv("TBG_RELAX_CHUNK", "200")
-    rep_c, st_c = _run(True, seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
+    rep_c, st_c = _run("relax", seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
     assert st_c["resolver_events"] > 0
     assert rep_r == rep_c
     rep_w, st_w = _run(False, seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)

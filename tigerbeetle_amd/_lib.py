@@ -45,6 +45,7 @@ FLAG_NO_COMPONENTS = 2
 FLAG_RES_WAIT = 4
 FLAG_CHANGE_LOG = 8
 FLAG_NO_XWIN = 16
+FLAG_NO_CHUNKS = 32
 
 
 class Stats(ctypes.Structure):
@@ -52,7 +53,7 @@ class Stats(ctypes.Structure):
                 ("expiry_entries", ctypes.c_uint64), ("pulse_next_timestamp", ctypes.c_uint64),
                 ("events_total", ctypes.c_uint64), ("walker_events", ctypes.c_uint64),
                 ("resolver_events", ctypes.c_uint64), ("component_events", ctypes.c_uint64),
-                ("sorted_transfers", ctypes.c_uint64)]
+                ("sorted_transfers", ctypes.c_uint64), ("chunked_windows", ctypes.c_uint64)]
 
 
 class Demuxer(ctypes.Structure):

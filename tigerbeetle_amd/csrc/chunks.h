@@ -1,0 +1,330 @@
+// chunks.h — chunked exact resolution of balance-limit windows in ONE workgroup (default resolver
+// when the window's hot accounts fit its LDS).
+//
+// Same class, equations and outputs as relax.h (the sequential execution, state_machine.zig:
+// 1220-1306 calling create_transfer's limit checks :1567-1570, is the unique solution of
+//   s[e] = AND over the sides of e that check: amount(e) <= A_side(e)
+//   A_x(e) = A_x(start) + effects on x of the committed events before e), solved chunk by chunk:
+//  * the window is cut into aligned chunks of RC_C events; the sorted entries are keyed by
+//    (chunk, compact hot rank), so a chunk's entries are contiguous and grouped by account;
+//  * one workgroup walks the chunks in order with every hot account's available balance A in LDS
+//    (exact at each chunk start); a chunk's entries, statuses and segment table live in LDS;
+//  * inside a chunk it iterates: every account segment is walked exactly in event order from A
+//    (a wave per long segment: 64-entry exclusive scan, then the first failing check corrected and
+//    the rest re-tested, as in relax.h; a lane per short one), reading the other side's check of
+//    the previous iteration (initially: pass); when no check that another walker reads changed,
+//    the chunk is the unique solution (every status is computed from the statuses it reads), so A
+//    advances by each segment's effects and the next chunk starts. Iteration k settles at least the
+//    chunk's first k positions, so a chunk needs at most RC_C + 1 iterations.
+// Cross-walker traffic is LDS only and a step is a workgroup barrier (sub-microsecond), against a
+// grid barrier per relax.h iteration: the cfg3 window (Zipf-hot accounts, ~2.5 % exceeds_credits)
+// needs ~2.6 iterations per 1024-event chunk. Eligible: at most RC_MAXR hot accounts after
+// k_bind_decide (compact ranks), window amounts below 2^62 (in-chunk sums in int64), E <= 2^20.
+// Outputs as relax.h: st[] pass bits (k_res_final), per-entry committed bits in rown[] (k_res_sum
+// then sums them per account, k_res_apply applies the sums).
+#pragma once
+#include "relax.h"
+
+#define RC_T 1024  // threads of the workgroup
+#define RC_ME (2 * RC_C)  // entries per chunk at most
+#define RC_LONG 8  // longer segments are walked by a whole wave
+#ifndef RC_DEBUG
+#define RC_DEBUG 0  // 1: bounds checks and a wall-clock bail-out recorded into Globals::dbg
+#endif
+
+// Sorted (chunk, rank) pairs -> entries (meta, amount), chunk boundaries rc_cb[0..nch], and per
+// rank its account slot and initial A (written by the first entry of each (chunk, rank) segment:
+// identical values).
+__global__ void __launch_bounds__(256) k_rc_segs(Dev d, Scratch s, uint32_t n, uint32_t nch) {
+  const Globals* g = d.g;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n || !g->res_chunked) return;
+  const uint32_t key = s.rkey[k];
+  const uint32_t cc = key == RC_DUMMY ? nch : key >> RC_RBITS;
+  uint32_t lo = 0;
+  if (k) {
+    const uint32_t kp = s.rkey[k - 1];
+    lo = (kp == RC_DUMMY ? nch : kp >> RC_RBITS) + 1u;
+  }
+  for (uint32_t c = lo; c <= cc; c++) s.rc_cb[c] = k;
+  if (k + 1 == n)
+    for (uint32_t c = cc + 1; c <= nch; c++) s.rc_cb[c] = n;
+  if (key == RC_DUMMY) return;
+  const uint32_t v = s.rval[k];
+  const uint32_t e = v >> 1, side = v & 1;
+  const uint32_t cls = s.cls[e];
+  const bool need_dr = cls & C_READS_DR, need_cr = cls & C_READS_CR;
+  const uint32_t slot = side ? s.cr_slot[e] : s.dr_slot[e];
+  const tb_account_t& a = d.acc[slot];
+  const bool dc = acc_is_dc(a.flags);
+  const bool pending = cls & C_PENDING;
+  const bool check = side ? need_cr : need_dr;
+  const bool add = !check && !pending && (side ? dc : !dc);
+  const bool wait = side ? need_dr : need_cr;
+  s.rmeta[k] = e | (side ? RM_SIDE : 0) | (check ? RM_CHECK : 0) | (wait ? RM_WAIT : 0) | (add ? RM_ADD : 0) |
+               (pending ? RM_PEND : 0);
+  s.ramt[k] = s.amt[e];
+  if (k == 0 || s.rkey[k - 1] != key) {
+    const __int128 dp = (__int128)U(a.debits_pending), dpo = (__int128)U(a.debits_posted);
+    const __int128 cp = (__int128)U(a.credits_pending), cpo = (__int128)U(a.credits_posted);
+    RState& rs = s.rstate[key & RC_RMASK];
+    rs.start = 0;
+    rs.end = 1;  // k_res_apply: the rank has entries
+    rs.slot = slot;
+    rs.A = dc ? cpo - dp - dpo : dpo - cp - cpo;
+    rs.d[0] = rs.d[1] = rs.d[2] = rs.d[3] = 0;
+  }
+}
+
+struct RcLds {
+  __int128 A[RC_MAXR];         // available balance of every hot rank at the current chunk start
+  uint64_t amt[RC_ME];         // the chunk's entries, grouped by rank, event order inside a rank
+  uint32_t meta[RC_ME];
+  int64_t delta[RC_ME];        // per segment: its effects on A in the last iteration
+  uint16_t rank[RC_ME];
+  uint16_t seg[RC_ME + 1];     // segment starts (entry index), seg[nseg] = entries
+  uint16_t lng[RC_ME], sht[RC_ME];  // long / short segment ids
+  uint8_t ok[RC_ME];           // entry's effect applies (the event commits)
+  uint8_t cur[2][RC_C], prv[2][RC_C];  // per side: this / last iteration's check (1 = pass)
+  uint8_t wt[2][RC_C];         // per side: another walker reads this side's check
+  uint32_t wcnt[2][RC_T / 64];
+  uint32_t nseg, nlong, nshort, qlong, qshort, bad;
+};
+
+__device__ inline int64_t rc_clamp(__int128 a) {
+  if (a > (__int128)INT64_MAX) return INT64_MAX;
+  if (a < (__int128)INT64_MIN) return INT64_MIN;
+  return (int64_t)a;
+}
+
+// Whole-wave walk of segment sg (64 entries per step). A check passes iff amount <= A0 + D + pre,
+// i.e. amount - (pre + D) <= A0: |pre + D| <= the window's amounts < 2^62, so the left side fits an
+// int64 and A0 is clamped into int64 without changing any comparison.
+__device__ inline uint32_t rc_uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+__device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t c0, int lane) {
+  // wave-uniform bounds (SGPRs): the step loop and its ballots are uniform control flow
+  const uint32_t s0 = rc_uniform(L.seg[sg]), s1 = rc_uniform(L.seg[sg + 1]);
+  const int64_t A0 = (int64_t)(((uint64_t)rc_uniform((uint32_t)((uint64_t)rc_clamp(L.A[L.rank[s0]]) >> 32)) << 32) |
+                               rc_uniform((uint32_t)(uint64_t)rc_clamp(L.A[L.rank[s0]])));
+  int64_t D = 0;
+  for (uint32_t k = s0; k < s1; k += 64) {
+    const uint32_t kk = k + (uint32_t)lane;
+    const bool act = kk < s1;
+    const uint32_t n = min(64u, s1 - k);
+    const uint32_t meta = act ? L.meta[kk] : 0u;
+    const int64_t amt = act ? (int64_t)L.amt[kk] : 0;
+    const uint32_t el = (meta & RM_EVENT) - c0;
+    const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
+    const bool check = meta & RM_CHECK;
+    const bool opass = !(meta & RM_WAIT) || L.prv[side ^ 1u][el & (RC_C - 1)];
+    bool ok = act && opass;
+    int64_t eff = 0;
+    if (ok) eff = check ? -amt : ((meta & RM_ADD) ? amt : 0);
+    int64_t pre = wave_incl_scan_i64(eff) - eff;
+    int floor_lane = -1;
+    for (;;) {
+      const unsigned long long fm = __ballot(ok && check && lane > floor_lane && amt - (pre + D) > A0);
+      if (!fm) break;
+      const int jl = __builtin_ctzll(fm);
+      const int64_t aj = readlane_i64(amt, jl);
+      if (lane > jl) pre += aj;
+      if (lane == jl) {
+        ok = false;
+        eff = 0;
+      }
+      floor_lane = jl;
+    }
+    if (RC_DEBUG && __any(act && el >= RC_C)) {  // (uniform exit)
+      if (act && el >= RC_C) L.bad = 0x1000000u | el;
+      break;
+    }
+    if (act) {
+      if (check) L.cur[side][el] = amt - (pre + D) <= A0 ? 1 : 0;
+      L.ok[kk] = ok ? 1 : 0;
+    }
+    D += readlane_i64(pre + eff, (int)n - 1);
+  }
+  if (lane == 0) L.delta[sg] = D;
+}
+
+// One lane walks segment sg entry by entry.
+__device__ inline void rc_walk_lane(RcLds& L, uint32_t sg, uint32_t c0) {
+  const uint32_t s0 = L.seg[sg], s1 = L.seg[sg + 1];
+  const int64_t A0 = rc_clamp(L.A[L.rank[s0]]);
+  int64_t D = 0;
+  for (uint32_t k = s0; k < s1; k++) {
+    const uint32_t meta = L.meta[k];
+    const int64_t amt = (int64_t)L.amt[k];
+    const uint32_t el = (meta & RM_EVENT) - c0;
+    const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
+    if (RC_DEBUG && el >= RC_C) {
+      L.bad = 0x2000000u | el;
+      break;
+    }
+    const bool opass = !(meta & RM_WAIT) || L.prv[side ^ 1u][el];
+    bool ok;
+    if (meta & RM_CHECK) {
+      const bool pass = amt - D <= A0;
+      L.cur[side][el] = pass ? 1 : 0;
+      ok = opass && pass;
+      if (ok) D -= amt;
+    } else {
+      ok = opass;
+      if (ok && (meta & RM_ADD)) D += amt;
+    }
+    L.ok[k] = ok ? 1 : 0;
+  }
+  L.delta[sg] = D;
+}
+
+__global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
+  __shared__ RcLds L;
+  Globals* g = d.g;
+  if (!g->res_chunked) return;
+  const uint32_t t = threadIdx.x;
+  const int lane = t & 63;
+  const uint32_t wave = t >> 6;
+  const uint32_t nch = (E + RC_C - 1) / RC_C;
+  const uint32_t R = g->hot_live;
+  for (uint32_t r = t; r < R; r += RC_T) L.A[r] = s.rstate[r].A;
+  // entries of the next chunk, loaded one chunk ahead (two per thread)
+  uint32_t pm[2] = {0, 0}, pk[2] = {0, 0};
+  uint64_t pa[2] = {0, 0};
+  auto fetch = [&](uint32_t c) {
+    const uint32_t b0 = s.rc_cb[c], b1 = s.rc_cb[c + 1];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t k = b0 + t + (uint32_t)j * RC_T;
+      if (k < b1) {
+        pm[j] = s.rmeta[k];
+        pk[j] = s.rkey[k];
+        pa[j] = (uint64_t)s.ramt[k];
+      }
+    }
+  };
+  fetch(0);
+  uint64_t iters = 0;
+  const uint64_t t_start = wall_clock64();
+  if (t == 0) L.bad = 0;
+  for (uint32_t c = 0; c < nch; c++) {
+    const uint32_t cb0 = s.rc_cb[c], m = s.rc_cb[c + 1] - cb0;
+    const uint32_t c0 = c * RC_C;
+    __syncthreads();  // the previous chunk's LDS is consumed
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t kl = t + (uint32_t)j * RC_T;
+      if (kl < m) {
+        L.meta[kl] = pm[j];
+        L.amt[kl] = pa[j];
+        L.rank[kl] = (uint16_t)(pk[j] & RC_RMASK);
+      }
+    }
+    L.wt[0][t] = L.wt[1][t] = 0;
+    L.prv[0][t] = L.prv[1][t] = 1;
+    if (t == 0) L.nlong = L.nshort = 0;
+    if (c + 1 < nch) fetch(c + 1);
+    if (m == 0) continue;
+    __syncthreads();
+    // segments: ordered compaction of the rank-change positions
+    bool f[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t kl = t + (uint32_t)j * RC_T;
+      f[j] = kl < m && (kl == 0 || L.rank[kl] != L.rank[kl - 1]);
+      if (kl < m && (L.meta[kl] & RM_WAIT)) {
+        const uint32_t meta = L.meta[kl];
+        L.wt[(meta & RM_SIDE) ? 0 : 1][(meta & RM_EVENT) - c0] = 1;  // this entry reads the other side
+      }
+    }
+    const unsigned long long b0 = __ballot(f[0]), b1 = __ballot(f[1]);
+    if (lane == 0) {
+      L.wcnt[0][wave] = (uint32_t)__popcll(b0);
+      L.wcnt[1][wave] = (uint32_t)__popcll(b1);
+    }
+    __syncthreads();
+    uint32_t pre0 = 0, tot0 = 0, pre1 = 0, tot1 = 0;
+    for (uint32_t w = 0; w < RC_T / 64; w++) {
+      const uint32_t a0 = L.wcnt[0][w], a1 = L.wcnt[1][w];
+      pre0 += w < wave ? a0 : 0u;
+      pre1 += w < wave ? a1 : 0u;
+      tot0 += a0;
+      tot1 += a1;
+    }
+    const unsigned long long below = (1ull << lane) - 1ull;
+    if (f[0]) L.seg[pre0 + (uint32_t)__popcll(b0 & below)] = (uint16_t)t;
+    if (f[1]) L.seg[tot0 + pre1 + (uint32_t)__popcll(b1 & below)] = (uint16_t)(t + RC_T);
+    const uint32_t nseg = tot0 + tot1;
+    if (t == 0) {
+      L.seg[nseg] = (uint16_t)m;
+      L.nseg = nseg;
+    }
+    __syncthreads();
+    for (uint32_t sg = t; sg < nseg; sg += RC_T) {
+      const bool lg = (uint32_t)(L.seg[sg + 1] - L.seg[sg]) > RC_LONG;
+      if (lg) L.lng[atomicAdd(&L.nlong, 1u)] = (uint16_t)sg;
+      else L.sht[atomicAdd(&L.nshort, 1u)] = (uint16_t)sg;
+    }
+    for (uint32_t it = 0;; it++) {
+      if (it > RC_C + 1) {  // cannot happen (see header); the sequential walker takes the window
+        if (t == 0) g->res_error = 1;
+        return;
+      }
+      L.cur[0][t] = L.cur[1][t] = 1;
+      if (t == 0) L.qlong = L.qshort = 0;
+      __syncthreads();
+      const uint32_t nlong = rc_uniform(L.nlong), nshort = rc_uniform(L.nshort);
+      // work queues: long segments one per wave, short ones 64 per wave (one per lane). Every lane
+      // of the wave adds 1 (one LDS atomic of 64 after the compiler's wave aggregation): the long
+      // queue counts 64 per grab, the short queue hands each lane its own index. No lane-divergent
+      // branch around the atomic, so the loops stay wave-uniform (a grab under `if (lane == 0)` let
+      // the compiler split the loop per lane and re-walk segment 0 forever).
+      for (;;) {
+        const uint32_t j = rc_uniform(atomicAdd(&L.qlong, 1u)) >> 6;
+        if (j >= nlong) break;
+        if (RC_DEBUG && wall_clock64() - t_start > 100000000ull) break;
+        rc_walk_wave(L, L.lng[j], c0, lane);
+      }
+      for (;;) {
+        const uint32_t j = atomicAdd(&L.qshort, 1u);
+        const uint32_t j0 = rc_uniform(j);
+        if (j0 >= nshort) break;
+        if (RC_DEBUG && wall_clock64() - t_start > 100000000ull) break;
+        if (j < nshort) rc_walk_lane(L, L.sht[j], c0);
+      }
+      __syncthreads();
+      const bool ch = (L.wt[0][t] && L.cur[0][t] != L.prv[0][t]) || (L.wt[1][t] && L.cur[1][t] != L.prv[1][t]);
+      L.prv[0][t] = L.cur[0][t];
+      L.prv[1][t] = L.cur[1][t];
+      iters++;
+      if (RC_DEBUG) {
+        const bool stop = L.bad || wall_clock64() - t_start > 100000000ull;
+        __syncthreads();
+        if (stop) {
+          if (t == 0) {
+            g->dbg[1] = ((uint64_t)c << 32) | it;
+            g->dbg[2] = ((uint64_t)m << 32) | L.nseg;
+            g->dbg[3] = ((uint64_t)nlong << 32) | nshort;
+            g->dbg[4] = ((uint64_t)L.qlong << 32) | L.qshort;
+            g->dbg[7] = L.bad;
+            g->res_error = 1;
+          }
+          return;
+        }
+      }
+      if (!__syncthreads_or(ch)) break;
+    }
+    // the chunk is final: advance A, publish the statuses and the committed entries
+    for (uint32_t sg = t; sg < nseg; sg += RC_T) L.A[L.rank[L.seg[sg]]] += (__int128)L.delta[sg];
+    if (c0 + t < E) s.st[c0 + t] = (L.cur[0][t] ? ST_DR_PASS : 0u) | (L.cur[1][t] ? ST_CR_PASS : 0u);
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t kl = t + (uint32_t)j * RC_T;
+      if (kl < m) s.rown[cb0 + kl] = L.ok[kl];
+    }
+  }
+  if (t == 0) {
+    g->dbg[0] += iters;
+    g->res_chunk_windows++;
+  }
+}

@@ -124,6 +124,11 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t final_done;  // k_final blocks finished in a window with pulse_next ops (the last runs k_pn)
   uint32_t pad4;
   uint64_t win_id_max;  // this window's largest transfer id key (k_ct_prep), folded into x_id_max
+  // chunked resolver (chunks.h), per window: hot accounts left after k_bind_decide (compact ranks
+  // 0..hot_live-1) and whether this window's resolver runs in chunked mode
+  uint32_t hot_live;
+  uint32_t res_chunked;
+  uint64_t res_chunk_windows;  // cumulative windows the chunked resolver decided
 };
 
 // Whether this block is the last of its grid to arrive (every thread of every block calls it once).

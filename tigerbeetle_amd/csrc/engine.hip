@@ -44,6 +44,7 @@ using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::def
 #include "walker.h"
 #include "resolver.h"
 #include "relax.h"
+#include "chunks.h"
 #include "window.h"
 #include "changes.h"
 #include "restore.h"
@@ -198,7 +199,17 @@ __global__ void __launch_bounds__(256) k_bind_decide(Dev d, Scratch s) {
     }
   }
   const unsigned long long m = __ballot(cold);
-  if (m && (threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(&g->cold_count, (uint32_t)__popcll(m));
+  const int lane = threadIdx.x & 63;
+  if (m && lane == __builtin_ctzll(m)) atomicAdd(&g->cold_count, (uint32_t)__popcll(m));
+  // the accounts that stay hot get compact ranks 0..hot_live-1 (the resolver's keys, chunks.h)
+  const unsigned long long live = __ballot(r < n && !cold);
+  if (live) {
+    const int leader = __builtin_ctzll(live);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&g->hot_live, (uint32_t)__popcll(live));
+    base = __shfl(base, leader, 64);
+    if (r < n && !cold) d.hot_rank[s.bind_slot[r]] = base + (uint32_t)__popcll(live & ((1ull << lane) - 1));
+  }
 }
 
 // Every hot account non-binding: the window reads no balance after all (cpw / order-free paths).
@@ -1292,6 +1303,8 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     }
     gw->windows_applied++;
     gw->hot_count = 0;
+    gw->hot_live = 0;
+    gw->res_chunked = 0;
     gw->res_inelig = 0;
     gw->res_error = 0;
     gw->res_done = 0;

@@ -358,7 +358,7 @@ __device__ inline uint32_t relax_visit(const Scratch& s, RSlot& q, uint32_t mark
 // the others the light ranks, one per lane.
 __global__ void __launch_bounds__(RELAX_THREADS) k_res_relax(Dev d, Scratch s, uint32_t E, uint32_t chunk) {
   Globals* g = d.g;
-  if (g->res_inelig || !g->hot_count) return;
+  if (g->res_inelig || !g->hot_count || g->res_chunked) return;
   const uint32_t H = g->heavy_count, L = g->light_count;
   const uint32_t P = gridDim.x * (RELAX_THREADS / 64);
   const uint32_t wave = blockIdx.x * (RELAX_THREADS / 64) + (threadIdx.x >> 6);
@@ -465,7 +465,7 @@ __global__ void __launch_bounds__(RELAX_THREADS) k_res_relax(Dev d, Scratch s, u
 // Per entry: the other side's entry of the same event and its rank (or NONE when that side is not hot).
 __global__ void __launch_bounds__(256) k_res_links(Dev d, Scratch s, uint32_t n) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n || d.g->res_inelig || !d.g->hot_count) return;
+  if (k >= n || d.g->res_inelig || !d.g->hot_count || d.g->res_chunked) return;
   if (s.rkey[k] == RES_DUMMY) return;
   const uint32_t v = s.rval[k];
   const uint32_t ko = s.kidx[v ^ 1u];
@@ -473,27 +473,34 @@ __global__ void __launch_bounds__(256) k_res_links(Dev d, Scratch s, uint32_t n)
 }
 
 // Per-account effect sums of the committed entries: a committed entry adds its amount to its
-// account's field rm_field(meta). Segmented wave sums by rank, one u128 atomic per segment.
+// account's field rm_field(meta). Segmented wave sums by key, one u128 atomic per segment.
+// CHUNKED (chunks.h): keys are (chunk, rank), rown holds each entry's committed bit, st is written.
+template <bool CHUNKED>
 __global__ void __launch_bounds__(256) k_res_sum(Dev d, Scratch s, uint32_t n) {
   const Globals* g = d.g;
-  if (g->res_inelig || !g->hot_count || g->res_error) return;
+  if (g->res_inelig || !g->hot_count || g->res_error || (g->res_chunked != 0) != CHUNKED) return;
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
-  uint32_t key = RES_DUMMY;
+  const uint32_t dummy = CHUNKED ? RC_DUMMY : RES_DUMMY;
+  uint32_t key = dummy;
   u128 v[4] = {0, 0, 0, 0};
   if (k < n) {
     key = s.rkey[k];
-    if (key != RES_DUMMY) {
+    if (key != dummy) {
       const uint32_t meta = s.rmeta[k];
-      const uint32_t e = meta & RM_EVENT;
-      const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
       bool ok = true;
-      if (meta & RM_CHECK) {
-        const bool pass = s.rown[k] == 1u;
-        atomicOr(&s.st[e], st_known(side) | (pass ? st_pass_bit(side) : 0u));  // for k_res_final
-        ok = pass;
+      if (CHUNKED) {
+        ok = s.rown[k] != 0u;
+      } else {
+        const uint32_t e = meta & RM_EVENT;
+        const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
+        if (meta & RM_CHECK) {
+          const bool pass = s.rown[k] == 1u;
+          atomicOr(&s.st[e], st_known(side) | (pass ? st_pass_bit(side) : 0u));  // for k_res_final
+          ok = pass;
+        }
+        if (meta & RM_WAIT) ok = ok && s.roth[k] != 0u;
       }
-      if (meta & RM_WAIT) ok = ok && s.roth[k] != 0u;
       if (ok) v[rm_field(meta)] = s.ramt[k];
     }
   }
@@ -513,8 +520,8 @@ __global__ void __launch_bounds__(256) k_res_sum(Dev d, Scratch s, uint32_t n) {
   }
   const uint32_t kn = (uint32_t)__shfl_down((int)key, 1, 64);
   const bool last = lane == 63 || kn != key || k + 1 >= n;
-  if (key != RES_DUMMY && k < n && last) {
-    RState& rs = s.rstate[key];
+  if (key != dummy && k < n && last) {
+    RState& rs = s.rstate[CHUNKED ? key & RC_RMASK : key];
 #pragma unroll
     for (int f = 0; f < 4; f++)
       if (v[f]) atomic_add_u128((tb_uint128_t*)&rs.d[f], v[f]);

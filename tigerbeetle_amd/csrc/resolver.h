@@ -39,6 +39,14 @@
 
 #define RES_KEY_BITS 21
 #define RES_DUMMY ((1u << RES_KEY_BITS) - 1)
+// chunked mode (chunks.h): keys (1024-event chunk << RC_RBITS | compact rank)
+#define RC_C 1024
+#define RC_RBITS 12
+#define RC_RMASK ((1u << RC_RBITS) - 1u)
+#define RC_MAXR RC_RMASK                         // compact ranks 0..RC_MAXR-1
+#define RC_DUMMY ((1u << (RC_RBITS + 10)) - 1u)  // sorts after every (chunk < 1024, rank) key
+#define RES_SORT_BITS (RC_RBITS + 10)            // the resolver's sort (>= RES_KEY_BITS)
+static_assert(RES_SORT_BITS >= RES_KEY_BITS, "sort bits");
 #define HEAVY_T 16
 
 enum : uint32_t { ST_DR_KNOWN = 1, ST_DR_PASS = 2, ST_CR_KNOWN = 4, ST_CR_PASS = 8 };
@@ -77,9 +85,16 @@ __device__ inline void st_publish(uint32_t* p, uint32_t bits) {
   __hip_atomic_fetch_or(p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Chunked mode: every hot account that k_bind_decide kept has a compact rank < RC_MAXR, the
+// window's amounts sum below 2^62 (in-chunk int64 sums) and E <= 2^20 (1024 chunks).
+__device__ inline bool rc_eligible(const Globals* g, uint32_t E) {
+  return !WIN_REJECTED(g) && g->hot_live && g->hot_live <= RC_MAXR && !g->batch_huge &&
+         g->batch_amount_sum < ((u128)1 << 62) && E <= 1024u * RC_C;
+}
+
 // Keys: one (hot rank, 2*event+side) pair per side of a W event (not failed in validation) whose
 // account is hot. Also zeroes the per-event status words and the per-rank segments.
-__global__ void __launch_bounds__(256) k_res_keys(Dev d, Scratch s, uint32_t E, uint32_t epoch) {
+__global__ void __launch_bounds__(256) k_res_keys(Dev d, Scratch s, uint32_t E, uint32_t epoch, uint32_t allow_chunks) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   Globals* g = d.g;
   const bool active = !g->res_inelig && g->hot_count;
@@ -92,17 +107,22 @@ __global__ void __launch_bounds__(256) k_res_keys(Dev d, Scratch s, uint32_t E, 
     g->res_bar_top = 0;
     g->res_fc[0] = NONE32;
   }
+  // chunked mode (chunks.h): keys (1024-event chunk, compact rank), else (rank)
+  const bool chunked = active && allow_chunks && rc_eligible(g, E);
+  if (i == 0) g->res_chunked = chunked ? 1u : 0u;
   if (i >= E) return;
   s.kidx[2 * i] = NONE32;
   s.kidx[2 * i + 1] = NONE32;
   s.st[i] = 0;
-  uint32_t key[2] = {RES_DUMMY, RES_DUMMY};
+  const uint32_t dummy = chunked ? RC_DUMMY : RES_DUMMY;
+  uint32_t key[2] = {dummy, dummy};
   if (active) {
     const uint32_t cls = s.cls[i];
     if ((cls & C_W) && s.code[i] == TB_CT_OK) {
       const uint32_t dr = s.dr_slot[i], cr = s.cr_slot[i];
-      if (d.hot[dr] == epoch) key[0] = d.hot_rank[dr];
-      if (d.hot[cr] == epoch) key[1] = d.hot_rank[cr];
+      const uint32_t hi = chunked ? (i / RC_C) << RC_RBITS : 0u;
+      if (d.hot[dr] == epoch) key[0] = hi | d.hot_rank[dr];
+      if (d.hot[cr] == epoch) key[1] = hi | d.hot_rank[cr];
     }
   }
   s.rkey_in[2 * i] = key[0];
@@ -114,7 +134,7 @@ __global__ void __launch_bounds__(256) k_res_keys(Dev d, Scratch s, uint32_t E, 
 // Sorted pairs -> entries (meta, amount) and per-rank segments with the account's initial A.
 __global__ void __launch_bounds__(256) k_res_segs(Dev d, Scratch s, uint32_t n) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n || d.g->res_inelig || !d.g->hot_count) return;
+  if (k >= n || d.g->res_inelig || !d.g->hot_count || d.g->res_chunked) return;
   const uint32_t key = s.rkey[k];
   if (key == RES_DUMMY) return;
   const uint32_t v = s.rval[k];
@@ -153,7 +173,7 @@ __global__ void __launch_bounds__(256) k_res_segs(Dev d, Scratch s, uint32_t n) 
 __global__ void __launch_bounds__(256) k_res_split(Dev d, Scratch s) {
   Globals* g = d.g;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g->res_inelig || r >= g->hot_count) return;
+  if (g->res_inelig || g->res_chunked || r >= g->hot_count) return;
   const uint32_t len = s.rstate[r].end - s.rstate[r].start;
   if (len == 0) return;
   const bool heavy = len > HEAVY_T;
@@ -404,7 +424,7 @@ __device__ inline bool lane_advance(const Scratch& s, uint32_t r, uint32_t budge
 // (lane-strided, round-robin when a lane owns several).
 __global__ void __launch_bounds__(RES_THREADS) k_res_walk(Dev d, Scratch s) {
   Globals* g = d.g;
-  if (g->res_inelig || !g->hot_count) return;
+  if (g->res_inelig || !g->hot_count || g->res_chunked) return;
   const uint32_t H = g->heavy_count, L = g->light_count;
   const uint32_t P = gridDim.x * (RES_THREADS / 64);
   const uint32_t wave = blockIdx.x * (RES_THREADS / 64) + (threadIdx.x >> 6);

@@ -109,6 +109,7 @@ struct Scratch {
   // (debits of a debits<=credits account, credits of a credits<=debits one; bit 63 = must stay hot)
   uint32_t* bind_slot;
   unsigned long long* bind_adv;
+  uint32_t* rc_cb;  // chunked resolver (chunks.h): first sorted entry of each 1024-event chunk
   // pulse_next (k_pn): per event the op's value (C_PNOP) and, for a walker post/void of a pending
   // transfer created in the window, that transfer's event index; per segment the min creation value
   // and the count of resets among the events that ran ok

@@ -60,6 +60,7 @@ __global__ void k_xwin_decide(Dev d, Scratch s, WinDesc w, uint32_t cap) {
   if (!bad) return;
   atomicOr(&g->window_error, 1u);
   g->hot_count = 0;
+  g->hot_live = 0;
   g->batch_amount_sum = 0;
   g->batch_huge = 0;
   g->res_inelig = 0;

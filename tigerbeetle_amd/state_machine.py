@@ -32,10 +32,12 @@ class StateMachine:
                  window_events_max=0, resolver=True, components=True, shard_count=0, shard_index=0,
                  change_log=False):
         L = _lib.lib()
-        # resolver: True/"relax" = windowed relaxation (relax.h), "wait" = wait-based walkers
-        # (resolver.h), False = sequential walker only
+        # resolver: True = chunked single-workgroup resolver (chunks.h) where the window fits it, else
+        # windowed relaxation (relax.h); "relax" = relaxation only; "wait" = wait-based walkers
+        # (resolver.h); False = sequential walker only
         flags = ((0 if resolver else _lib.FLAG_NO_RESOLVER) | (0 if components else _lib.FLAG_NO_COMPONENTS) |
-                 (_lib.FLAG_RES_WAIT if resolver == "wait" else 0) | (_lib.FLAG_CHANGE_LOG if change_log else 0))
+                 (_lib.FLAG_RES_WAIT if resolver == "wait" else 0) |
+                 (_lib.FLAG_NO_CHUNKS if resolver == "relax" else 0) | (_lib.FLAG_CHANGE_LOG if change_log else 0))
         cfg = _lib.Config(device, batch_max, accounts_max, transfers_max, window_events_max, flags, shard_count,
                           shard_index)
         h = ctypes.c_void_p()

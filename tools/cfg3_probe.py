@@ -64,7 +64,8 @@ def main():
         L.tbg_debug_counters(sm.h, dbg, 8)
         L.tbg_timing_collect(sm.h, ms, cnt, len(PHASES))
         cur = list(dbg)
-        print(f"window {w}: iterations {cur[0] - prev[0]}, change-free {cur[1] - prev[1]}, failed {fails}")
+        print(f"window {w}: iterations {cur[0] - prev[0]}, change-free {cur[1] - prev[1]}, failed {fails}, "
+              f"dbg[2:8] {[cur[k] - prev[k] for k in range(2, 8)]}")
         print("   phases us: " + ", ".join(f"{p} {ms[k] * 1000:.0f}" for k, p in enumerate(PHASES) if cnt[k]))
         prev = cur
     print("stats", sm.stats())
