@@ -28,9 +28,10 @@
 #define RC_T 1024  // threads of the workgroup
 #define RC_ME (2 * RC_C)  // entries per chunk at most
 #define RC_LONG 8  // longer segments are walked by a whole wave
-#ifndef RC_DEBUG
-#define RC_DEBUG 0  // 1: bounds checks and a wall-clock bail-out recorded into Globals::dbg
+#ifndef RC_PROF
+#define RC_PROF 0  // 1: per-phase clock64() sums of k_rc_run into Globals::dbg (tbg_debug_counters)
 #endif
+#define RC_NONE 0xFFFFu
 
 // Sorted (chunk, rank) pairs -> entries (meta, amount), chunk boundaries rc_cb[0..nch], and per
 // rank its account slot and initial A (written by the first entry of each (chunk, rank) segment:
@@ -77,51 +78,70 @@ __global__ void __launch_bounds__(256) k_rc_segs(Dev d, Scratch s, uint32_t n, u
 }
 
 struct RcLds {
-  __int128 A[RC_MAXR];         // available balance of every hot rank at the current chunk start
+  int64_t A[RC_MAXR];          // available balance of every hot rank at the chunk start (clamped, below)
   uint64_t amt[RC_ME];         // the chunk's entries, grouped by rank, event order inside a rank
+  int64_t dent[RC_ME];         // per entry: the segment's effects on A before it (last walk)
+  int64_t delta[RC_ME];        // per segment: its effects on A (last walk)
   uint32_t meta[RC_ME];
-  int64_t delta[RC_ME];        // per segment: its effects on A in the last iteration
+  uint32_t dfrom[RC_ME];       // per segment: first entry whose input changed (RC_NONE: clean)
   uint16_t rank[RC_ME];
+  uint16_t segof[RC_ME];       // entry -> segment
   uint16_t seg[RC_ME + 1];     // segment starts (entry index), seg[nseg] = entries
-  uint16_t lng[RC_ME], sht[RC_ME];  // long / short segment ids
+  uint16_t lng[RC_ME];         // long segments: > 64 entries from the front, the others from the back
+  uint16_t sht[RC_ME];         // short segments
+  uint16_t ent[2][RC_C];       // per side and event: its entry (RC_NONE: that side is not hot)
   uint8_t ok[RC_ME];           // entry's effect applies (the event commits)
-  uint8_t cur[2][RC_C], prv[2][RC_C];  // per side: this / last iteration's check (1 = pass)
-  uint8_t wt[2][RC_C];         // per side: another walker reads this side's check
+  uint8_t oth[RC_ME];          // per entry: the other side's check as its reader sees it (1 = pass)
+  uint8_t cur[2][RC_C], prv[2][RC_C];  // per side: latest check / the one readers use (1 = pass)
+  uint32_t cb[1024 + 1];        // first entry of every chunk (no global load on a chunk's critical path)
   uint32_t wcnt[2][RC_T / 64];
-  uint32_t nseg, nlong, nshort, qlong, qshort, bad;
+  uint32_t nseg, nhuge, nlong, nshort, qlong, qshort, chg[2];
 };
 
+// A is kept clamped into int64: every decision compares amount - (pre + D) with it, where amount and
+// |pre + D| (a segment's effects, bounded by the window's amounts) are below 2^62, so a clamped value
+// decides exactly as the exact one; and A + delta of a clamped A stays beyond +-2^62, on the same side
+// of every comparison (the exact balances are applied by k_res_sum / k_res_apply, not from A).
 __device__ inline int64_t rc_clamp(__int128 a) {
   if (a > (__int128)INT64_MAX) return INT64_MAX;
   if (a < (__int128)INT64_MIN) return INT64_MIN;
   return (int64_t)a;
 }
+__device__ inline int64_t rc_sat_add(int64_t a, int64_t b) {
+  int64_t r;
+  if (__builtin_add_overflow(a, b, &r)) return a > 0 ? INT64_MAX : INT64_MIN;
+  return r;
+}
 
-// Whole-wave walk of segment sg (64 entries per step). A check passes iff amount <= A0 + D + pre,
-// i.e. amount - (pre + D) <= A0: |pre + D| <= the window's amounts < 2^62, so the left side fits an
-// int64 and A0 is clamped into int64 without changing any comparison.
 __device__ inline uint32_t rc_uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ inline int64_t rc_uniform64(int64_t v) {
+  return (int64_t)(((uint64_t)rc_uniform((uint32_t)((uint64_t)v >> 32)) << 32) | rc_uniform((uint32_t)(uint64_t)v));
+}
 
-__device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t c0, int lane) {
+// Whole-wave walk of segment sg from entry kf (64 entries per step). A check passes iff
+// amount <= A0 + D + pre, i.e. amount - (pre + D) <= A0. Re-walks start at the first entry whose
+// input changed, from the D recorded before it by the previous walk.
+__device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t kf, uint32_t c0, int lane) {
   // wave-uniform bounds (SGPRs): the step loop and its ballots are uniform control flow
-  const uint32_t s0 = rc_uniform(L.seg[sg]), s1 = rc_uniform(L.seg[sg + 1]);
-  const int64_t A0 = (int64_t)(((uint64_t)rc_uniform((uint32_t)((uint64_t)rc_clamp(L.A[L.rank[s0]]) >> 32)) << 32) |
-                               rc_uniform((uint32_t)(uint64_t)rc_clamp(L.A[L.rank[s0]])));
-  int64_t D = 0;
-  for (uint32_t k = s0; k < s1; k += 64) {
+  const uint32_t s1 = rc_uniform(L.seg[sg + 1]);
+  const int64_t A0 = rc_uniform64(L.A[L.rank[kf]]);
+  int64_t D = rc_uniform64(kf == rc_uniform(L.seg[sg]) ? 0 : L.dent[kf]);
+  for (uint32_t k = kf; k < s1; k += 64) {
     const uint32_t kk = k + (uint32_t)lane;
     const bool act = kk < s1;
     const uint32_t n = min(64u, s1 - k);
     const uint32_t meta = act ? L.meta[kk] : 0u;
     const int64_t amt = act ? (int64_t)L.amt[kk] : 0;
-    const uint32_t el = (meta & RM_EVENT) - c0;
+    const uint32_t el = ((meta & RM_EVENT) - c0) & (RC_C - 1);
     const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
     const bool check = meta & RM_CHECK;
-    const bool opass = !(meta & RM_WAIT) || L.prv[side ^ 1u][el & (RC_C - 1)];
+    const bool opass = L.oth[kk & (RC_ME - 1)];  // 1 unless the other side's check failed
     bool ok = act && opass;
     int64_t eff = 0;
     if (ok) eff = check ? -amt : ((meta & RM_ADD) ? amt : 0);
     int64_t pre = wave_incl_scan_i64(eff) - eff;
+    // the first failing check fails; take it out and re-test the later lanes; repeat (a failed
+    // debit only raises what later entries see, so each round settles one failure)
     int floor_lane = -1;
     for (;;) {
       const unsigned long long fm = __ballot(ok && check && lane > floor_lane && amt - (pre + D) > A0);
@@ -135,34 +155,28 @@ __device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t c0, int lane
       }
       floor_lane = jl;
     }
-    if (RC_DEBUG && __any(act && el >= RC_C)) {  // (uniform exit)
-      if (act && el >= RC_C) L.bad = 0x1000000u | el;
-      break;
-    }
     if (act) {
       if (check) L.cur[side][el] = amt - (pre + D) <= A0 ? 1 : 0;
       L.ok[kk] = ok ? 1 : 0;
+      L.dent[kk] = D + pre;
     }
     D += readlane_i64(pre + eff, (int)n - 1);
   }
   if (lane == 0) L.delta[sg] = D;
 }
 
-// One lane walks segment sg entry by entry.
-__device__ inline void rc_walk_lane(RcLds& L, uint32_t sg, uint32_t c0) {
-  const uint32_t s0 = L.seg[sg], s1 = L.seg[sg + 1];
-  const int64_t A0 = rc_clamp(L.A[L.rank[s0]]);
-  int64_t D = 0;
-  for (uint32_t k = s0; k < s1; k++) {
+// One lane walks segment sg from entry kf.
+__device__ inline void rc_walk_lane(RcLds& L, uint32_t sg, uint32_t kf, uint32_t c0) {
+  const uint32_t s1 = L.seg[sg + 1];
+  const int64_t A0 = L.A[L.rank[kf]];
+  int64_t D = kf == L.seg[sg] ? 0 : L.dent[kf];
+  for (uint32_t k = kf; k < s1; k++) {
     const uint32_t meta = L.meta[k];
     const int64_t amt = (int64_t)L.amt[k];
-    const uint32_t el = (meta & RM_EVENT) - c0;
+    const uint32_t el = ((meta & RM_EVENT) - c0) & (RC_C - 1);
     const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
-    if (RC_DEBUG && el >= RC_C) {
-      L.bad = 0x2000000u | el;
-      break;
-    }
-    const bool opass = !(meta & RM_WAIT) || L.prv[side ^ 1u][el];
+    const bool opass = L.oth[k];
+    L.dent[k] = D;
     bool ok;
     if (meta & RM_CHECK) {
       const bool pass = amt - D <= A0;
@@ -178,6 +192,12 @@ __device__ inline void rc_walk_lane(RcLds& L, uint32_t sg, uint32_t c0) {
   L.delta[sg] = D;
 }
 
+#define RC_T0() const uint64_t _rc0 = RC_PROF ? clock64() : 0
+#define RC_ADD(k, t0)                          \
+  do {                                         \
+    if (RC_PROF && t == 0) prof[k] += clock64() - (t0); \
+  } while (0)
+
 __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   __shared__ RcLds L;
   Globals* g = d.g;
@@ -187,12 +207,15 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   const uint32_t wave = t >> 6;
   const uint32_t nch = (E + RC_C - 1) / RC_C;
   const uint32_t R = g->hot_live;
-  for (uint32_t r = t; r < R; r += RC_T) L.A[r] = s.rstate[r].A;
+  uint64_t prof[4] = {0, 0, 0, 0};  // RC_PROF (thread 0): setup, walks, change detection cycles; walks
+  for (uint32_t r = t; r < R; r += RC_T) L.A[r] = rc_clamp(s.rstate[r].A);
+  for (uint32_t c = t; c <= nch; c += RC_T) L.cb[c] = s.rc_cb[c];
+  __syncthreads();
   // entries of the next chunk, loaded one chunk ahead (two per thread)
   uint32_t pm[2] = {0, 0}, pk[2] = {0, 0};
   uint64_t pa[2] = {0, 0};
   auto fetch = [&](uint32_t c) {
-    const uint32_t b0 = s.rc_cb[c], b1 = s.rc_cb[c + 1];
+    const uint32_t b0 = L.cb[c], b1 = L.cb[c + 1];
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       const uint32_t k = b0 + t + (uint32_t)j * RC_T;
@@ -205,12 +228,11 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   };
   fetch(0);
   uint64_t iters = 0;
-  const uint64_t t_start = wall_clock64();
-  if (t == 0) L.bad = 0;
   for (uint32_t c = 0; c < nch; c++) {
-    const uint32_t cb0 = s.rc_cb[c], m = s.rc_cb[c + 1] - cb0;
+    const uint32_t cb0 = L.cb[c], m = L.cb[c + 1] - cb0;
     const uint32_t c0 = c * RC_C;
     __syncthreads();  // the previous chunk's LDS is consumed
+    const uint64_t tp0 = RC_PROF ? clock64() : 0;
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       const uint32_t kl = t + (uint32_t)j * RC_T;
@@ -218,23 +240,30 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
         L.meta[kl] = pm[j];
         L.amt[kl] = pa[j];
         L.rank[kl] = (uint16_t)(pk[j] & RC_RMASK);
+        L.oth[kl] = 1;
       }
     }
-    L.wt[0][t] = L.wt[1][t] = 0;
+    L.ent[0][t] = L.ent[1][t] = RC_NONE;
+    L.cur[0][t] = L.cur[1][t] = 1;
     L.prv[0][t] = L.prv[1][t] = 1;
-    if (t == 0) L.nlong = L.nshort = 0;
+    if (t == 0) {
+      L.nhuge = L.nlong = L.nshort = 0;
+      L.qlong = L.qshort = 0;
+      L.chg[0] = L.chg[1] = 0;
+    }
     if (c + 1 < nch) fetch(c + 1);
     if (m == 0) continue;
     __syncthreads();
-    // segments: ordered compaction of the rank-change positions
+    // segments: ordered compaction of the rank-change positions; each entry's segment id is the
+    // count of starts up to it
     bool f[2];
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       const uint32_t kl = t + (uint32_t)j * RC_T;
       f[j] = kl < m && (kl == 0 || L.rank[kl] != L.rank[kl - 1]);
-      if (kl < m && (L.meta[kl] & RM_WAIT)) {
+      if (kl < m) {
         const uint32_t meta = L.meta[kl];
-        L.wt[(meta & RM_SIDE) ? 0 : 1][(meta & RM_EVENT) - c0] = 1;  // this entry reads the other side
+        L.ent[(meta & RM_SIDE) ? 1 : 0][(meta & RM_EVENT) - c0] = (uint16_t)kl;
       }
     }
     const unsigned long long b0 = __ballot(f[0]), b1 = __ballot(f[1]);
@@ -251,9 +280,13 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
       tot0 += a0;
       tot1 += a1;
     }
-    const unsigned long long below = (1ull << lane) - 1ull;
-    if (f[0]) L.seg[pre0 + (uint32_t)__popcll(b0 & below)] = (uint16_t)t;
-    if (f[1]) L.seg[tot0 + pre1 + (uint32_t)__popcll(b1 & below)] = (uint16_t)(t + RC_T);
+    const unsigned long long upto = (2ull << lane) - 1ull;  // lanes <= this one
+    const uint32_t id0 = pre0 + (uint32_t)__popcll(b0 & upto) - 1u;
+    const uint32_t id1 = tot0 + pre1 + (uint32_t)__popcll(b1 & upto) - 1u;
+    if (f[0]) L.seg[id0] = (uint16_t)t;
+    if (f[1]) L.seg[id1] = (uint16_t)(t + RC_T);
+    if (t < m) L.segof[t] = (uint16_t)id0;
+    if (t + RC_T < m) L.segof[t + RC_T] = (uint16_t)id1;
     const uint32_t nseg = tot0 + tot1;
     if (t == 0) {
       L.seg[nseg] = (uint16_t)m;
@@ -261,61 +294,81 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
     }
     __syncthreads();
     for (uint32_t sg = t; sg < nseg; sg += RC_T) {
-      const bool lg = (uint32_t)(L.seg[sg + 1] - L.seg[sg]) > RC_LONG;
-      if (lg) L.lng[atomicAdd(&L.nlong, 1u)] = (uint16_t)sg;
+      const uint32_t len = (uint32_t)(L.seg[sg + 1] - L.seg[sg]);
+      L.dfrom[sg] = L.seg[sg];  // every segment is walked in the first iteration
+      if (len > 64) L.lng[atomicAdd(&L.nhuge, 1u)] = (uint16_t)sg;
+      else if (len > RC_LONG) L.lng[RC_ME - 1u - atomicAdd(&L.nlong, 1u)] = (uint16_t)sg;
       else L.sht[atomicAdd(&L.nshort, 1u)] = (uint16_t)sg;
     }
+    __syncthreads();
+    RC_ADD(0, tp0);
+    const uint32_t nhuge = rc_uniform(L.nhuge), nlong = nhuge + rc_uniform(L.nlong), nshort = rc_uniform(L.nshort);
     for (uint32_t it = 0;; it++) {
       if (it > RC_C + 1) {  // cannot happen (see header); the sequential walker takes the window
         if (t == 0) g->res_error = 1;
         return;
       }
-      L.cur[0][t] = L.cur[1][t] = 1;
-      if (t == 0) L.qlong = L.qshort = 0;
-      __syncthreads();
-      const uint32_t nlong = rc_uniform(L.nlong), nshort = rc_uniform(L.nshort);
-      // work queues: long segments one per wave, short ones 64 per wave (one per lane). Every lane
-      // of the wave adds 1 (one LDS atomic of 64 after the compiler's wave aggregation): the long
-      // queue counts 64 per grab, the short queue hands each lane its own index. No lane-divergent
-      // branch around the atomic, so the loops stay wave-uniform (a grab under `if (lane == 0)` let
-      // the compiler split the loop per lane and re-walk segment 0 forever).
+      const uint64_t tw0 = RC_PROF ? clock64() : 0;
+      // the dirty segments, from their first changed entry: long ones one per wave (the longest
+      // first), short ones one per lane. Every lane of the wave adds 1 (one LDS atomic of 64 after the
+      // compiler's wave aggregation): the long queue counts 64 per grab, the short queue hands each
+      // lane its own index. No lane-divergent branch around the atomic, so the loops stay
+      // wave-uniform (a grab under `if (lane == 0)` let the compiler split the loop per lane).
       for (;;) {
         const uint32_t j = rc_uniform(atomicAdd(&L.qlong, 1u)) >> 6;
         if (j >= nlong) break;
-        if (RC_DEBUG && wall_clock64() - t_start > 100000000ull) break;
-        rc_walk_wave(L, L.lng[j], c0, lane);
+        const uint32_t sg = rc_uniform(j < nhuge ? L.lng[j] : L.lng[RC_ME - 1u - (j - nhuge)]);
+        const uint32_t kf = rc_uniform(L.dfrom[sg]);
+        if (kf == RC_NONE) continue;
+        L.dfrom[sg] = RC_NONE;
+        rc_walk_wave(L, sg, kf, c0, lane);
+        if (RC_PROF && t == 0) prof[3]++;
       }
       for (;;) {
         const uint32_t j = atomicAdd(&L.qshort, 1u);
-        const uint32_t j0 = rc_uniform(j);
-        if (j0 >= nshort) break;
-        if (RC_DEBUG && wall_clock64() - t_start > 100000000ull) break;
-        if (j < nshort) rc_walk_lane(L, L.sht[j], c0);
-      }
-      __syncthreads();
-      const bool ch = (L.wt[0][t] && L.cur[0][t] != L.prv[0][t]) || (L.wt[1][t] && L.cur[1][t] != L.prv[1][t]);
-      L.prv[0][t] = L.cur[0][t];
-      L.prv[1][t] = L.cur[1][t];
-      iters++;
-      if (RC_DEBUG) {
-        const bool stop = L.bad || wall_clock64() - t_start > 100000000ull;
-        __syncthreads();
-        if (stop) {
-          if (t == 0) {
-            g->dbg[1] = ((uint64_t)c << 32) | it;
-            g->dbg[2] = ((uint64_t)m << 32) | L.nseg;
-            g->dbg[3] = ((uint64_t)nlong << 32) | nshort;
-            g->dbg[4] = ((uint64_t)L.qlong << 32) | L.qshort;
-            g->dbg[7] = L.bad;
-            g->res_error = 1;
+        if (rc_uniform(j) >= nshort) break;
+        if (j < nshort) {
+          const uint32_t sg = L.sht[j];
+          const uint32_t kf = L.dfrom[sg];
+          if (kf != RC_NONE) {
+            L.dfrom[sg] = RC_NONE;
+            rc_walk_lane(L, sg, kf, c0);
           }
-          return;
         }
       }
-      if (!__syncthreads_or(ch)) break;
+      __syncthreads();
+      RC_ADD(1, tw0);
+      const uint64_t td0 = RC_PROF ? clock64() : 0;
+      // changed checks mark their readers' segments dirty from the reading entry
+      if (t == 0) {
+        L.qlong = L.qshort = 0;
+        L.chg[(it + 1) & 1] = 0;
+      }
+      bool ch = false;
+#pragma unroll
+      for (int sd = 0; sd < 2; sd++) {
+        const uint8_t v = L.cur[sd][t];
+        if (v != L.prv[sd][t]) {
+          L.prv[sd][t] = v;
+          const uint32_t r = L.ent[sd ^ 1][t];
+          if (r != RC_NONE) {
+            L.oth[r] = v;
+            atomicMin(&L.dfrom[L.segof[r]], r);
+            ch = true;
+          }
+        }
+      }
+      if (ch) L.chg[it & 1] = 1;
+      iters++;
+      __syncthreads();
+      RC_ADD(2, td0);
+      if (!L.chg[it & 1]) break;
     }
     // the chunk is final: advance A, publish the statuses and the committed entries
-    for (uint32_t sg = t; sg < nseg; sg += RC_T) L.A[L.rank[L.seg[sg]]] += (__int128)L.delta[sg];
+    for (uint32_t sg = t; sg < nseg; sg += RC_T) {
+      const uint32_t r = L.rank[L.seg[sg]];
+      L.A[r] = rc_sat_add(L.A[r], L.delta[sg]);
+    }
     if (c0 + t < E) s.st[c0 + t] = (L.cur[0][t] ? ST_DR_PASS : 0u) | (L.cur[1][t] ? ST_CR_PASS : 0u);
 #pragma unroll
     for (int j = 0; j < 2; j++) {
@@ -325,6 +378,8 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   }
   if (t == 0) {
     g->dbg[0] += iters;
+    if (RC_PROF)
+      for (int k = 0; k < 4; k++) g->dbg[2 + k] += prof[k];
     g->res_chunk_windows++;
   }
 }

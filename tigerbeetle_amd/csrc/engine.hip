@@ -760,6 +760,11 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
   uint32_t v = 0;
   for (uint32_t j = threadIdx.x; j < nseg; j += WALK_THREADS) v += s.cnt_w[j];
   const uint32_t w_count = block_sum<WALK_THREADS / 64>(v, lds);
+  if (threadIdx.x == 0) {
+    // the host launches the component walkers only while recent windows had W events they could
+    // take (no hot account): balance-limit windows (resolver) skip their launches and sort
+    d.g->cpw_want = w_count != 0 && cpw_active(d.g) ? 1u : 0u;
+  }
   if (w_count == 0) {
     if (threadIdx.x == 0) {
       d.g->events_total += w.E;
