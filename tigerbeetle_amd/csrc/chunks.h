@@ -77,6 +77,13 @@ __global__ void __launch_bounds__(256) k_rc_segs(Dev d, Scratch s, uint32_t n, u
   }
 }
 
+// Per chunk, precomputed by k_rc_prep (one workgroup per chunk, all chunks at once) so that the
+// single workgroup of k_rc_run only copies a chunk's tables into LDS (one barrier per chunk):
+//   rc_segof[k]        entry k's segment within its chunk
+//   rc_seg[cb + c + i] segment i's first entry (i <= nseg; the last = the chunk's entry count)
+//   rc_list[cb + i]    segment ids: the > 64-entry segments, then the > RC_LONG ones, then the rest
+//   rc_ent[2e + side]  the entry of (event e, side) within its chunk (RC_NONE: that side is not hot)
+//   rc_cnt[c]          (nseg, huge, long, some amount >= 2^24)
 struct RcLds {
   int64_t A[RC_MAXR];          // available balance of every hot rank at the chunk start (clamped, below)
   uint64_t amt[RC_ME];         // the chunk's entries, grouped by rank, event order inside a rank
@@ -87,16 +94,95 @@ struct RcLds {
   uint16_t rank[RC_ME];
   uint16_t segof[RC_ME];       // entry -> segment
   uint16_t seg[RC_ME + 1];     // segment starts (entry index), seg[nseg] = entries
-  uint16_t lng[RC_ME];         // long segments: > 64 entries from the front, the others from the back
-  uint16_t sht[RC_ME];         // short segments
+  uint16_t lst[RC_ME];         // segment ids: long ones (the longest first), then short ones
   uint16_t ent[2][RC_C];       // per side and event: its entry (RC_NONE: that side is not hot)
   uint8_t ok[RC_ME];           // entry's effect applies (the event commits)
   uint8_t oth[RC_ME];          // per entry: the other side's check as its reader sees it (1 = pass)
   uint8_t cur[2][RC_C], prv[2][RC_C];  // per side: latest check / the one readers use (1 = pass)
   uint32_t cb[1024 + 1];        // first entry of every chunk (no global load on a chunk's critical path)
-  uint32_t wcnt[2][RC_T / 64];
-  uint32_t nseg, nhuge, nlong, nshort, qlong, qshort, chg[2];
+  uint32_t qlong, qshort, chg[2];
+  uint32_t pmax;  // RC_PROF: longest wave walk of the iteration (cycles)
 };
+
+__global__ void __launch_bounds__(RC_T) k_rc_prep(Dev d, Scratch s, uint32_t E) {
+  __shared__ uint16_t rank[RC_ME];
+  __shared__ uint16_t seg[RC_ME + 1];
+  __shared__ uint32_t wcnt[2][RC_T / 64];
+  __shared__ uint32_t ncls[3], big;
+  if (!d.g->res_chunked) return;
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  const int lane = t & 63;
+  const uint32_t wave = t >> 6;
+  const uint32_t cb0 = s.rc_cb[c], m = s.rc_cb[c + 1] - cb0, c0 = c * RC_C;
+  if (c0 + t < E) *(uint32_t*)&s.rc_ent[2 * (c0 + t)] = (RC_NONE << 16) | RC_NONE;
+  if (t < 3) ncls[t] = 0;
+  if (t == 0) big = 0;
+  bool bg = false;
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const uint32_t kl = t + (uint32_t)j * RC_T;
+    if (kl < m) {
+      rank[kl] = (uint16_t)(s.rkey[cb0 + kl] & RC_RMASK);
+      bg = bg || (uint64_t)s.ramt[cb0 + kl] >= (1ull << 24);
+    }
+  }
+  if (bg) big = 1;
+  __syncthreads();
+  bool f[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const uint32_t kl = t + (uint32_t)j * RC_T;
+    f[j] = kl < m && (kl == 0 || rank[kl] != rank[kl - 1]);
+    if (kl < m) {
+      const uint32_t meta = s.rmeta[cb0 + kl];
+      s.rc_ent[2 * (meta & RM_EVENT) + ((meta & RM_SIDE) ? 1 : 0)] = (uint16_t)kl;
+    }
+  }
+  const unsigned long long b0 = __ballot(f[0]), b1 = __ballot(f[1]);
+  if (lane == 0) {
+    wcnt[0][wave] = (uint32_t)__popcll(b0);
+    wcnt[1][wave] = (uint32_t)__popcll(b1);
+  }
+  __syncthreads();
+  uint32_t pre0 = 0, tot0 = 0, pre1 = 0, tot1 = 0;
+  for (uint32_t w = 0; w < RC_T / 64; w++) {
+    const uint32_t a0 = wcnt[0][w], a1 = wcnt[1][w];
+    pre0 += w < wave ? a0 : 0u;
+    pre1 += w < wave ? a1 : 0u;
+    tot0 += a0;
+    tot1 += a1;
+  }
+  const unsigned long long upto = (2ull << lane) - 1ull;  // lanes <= this one
+  const uint32_t id0 = pre0 + (uint32_t)__popcll(b0 & upto) - 1u;
+  const uint32_t id1 = tot0 + pre1 + (uint32_t)__popcll(b1 & upto) - 1u;
+  if (f[0]) seg[id0] = (uint16_t)t;
+  if (f[1]) seg[id1] = (uint16_t)(t + RC_T);
+  if (t < m) s.rc_segof[cb0 + t] = (uint16_t)id0;
+  if (t + RC_T < m) s.rc_segof[cb0 + t + RC_T] = (uint16_t)id1;
+  const uint32_t nseg = tot0 + tot1;
+  if (t == 0) seg[nseg] = (uint16_t)m;
+  __syncthreads();
+  uint32_t cls[2], idx[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const uint32_t sg = t + (uint32_t)j * RC_T;
+    cls[j] = 3;
+    if (sg <= nseg) s.rc_seg[cb0 + c + sg] = seg[sg];
+    if (sg < nseg) {
+      const uint32_t len = (uint32_t)(seg[sg + 1] - seg[sg]);
+      cls[j] = len > 64 ? 0u : (len > RC_LONG ? 1u : 2u);
+      idx[j] = atomicAdd(&ncls[cls[j]], 1u);
+    }
+  }
+  __syncthreads();
+  const uint32_t nh = ncls[0], nl = ncls[1];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const uint32_t sg = t + (uint32_t)j * RC_T;
+    if (cls[j] < 3) s.rc_list[cb0 + (cls[j] == 0 ? 0u : (cls[j] == 1 ? nh : nh + nl)) + idx[j]] = (uint16_t)sg;
+  }
+  if (t == 0) s.rc_cnt[c] = make_uint4(nseg, nh, nl, big);
+}
 
 // A is kept clamped into int64: every decision compares amount - (pre + D) with it, where amount and
 // |pre + D| (a segment's effects, bounded by the window's amounts) are below 2^62, so a clamped value
@@ -116,6 +202,87 @@ __device__ inline int64_t rc_sat_add(int64_t a, int64_t b) {
 __device__ inline uint32_t rc_uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ inline int64_t rc_uniform64(int64_t v) {
   return (int64_t)(((uint64_t)rc_uniform((uint32_t)((uint64_t)v >> 32)) << 32) | rc_uniform((uint32_t)(uint64_t)v));
+}
+
+// Inclusive wave64 scan of int32 (DPP row shifts, row broadcasts).
+__device__ inline int32_t wave_incl_scan_i32(int32_t x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
+// Whole-wave walk of a segment whose amounts are all below 2^24 (the chunk's common case): the
+// in-step prefix and amount - prefix fit an int32 (|.| < 65 * 2^24), and a check fails iff
+// amount - pre > A0 + D, with A0 + D clamped into int32 without changing any comparison. Same
+// outputs as rc_walk_wave.
+__device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, uint32_t c0, int lane, uint64_t& rounds,
+                                      uint64_t* tp) {
+  const uint32_t s1 = rc_uniform(L.seg[sg + 1]);
+  const int64_t A0 = rc_uniform64(L.A[L.rank[kf]]);
+  int64_t D = rc_uniform64(kf == rc_uniform(L.seg[sg]) ? 0 : L.dent[kf]);
+  for (uint32_t k = kf; k < s1; k += 64) {
+    const uint64_t q0 = RC_PROF ? clock64() : 0;
+    const uint32_t kk = k + (uint32_t)lane;
+    const bool act = kk < s1;
+    const uint32_t n = min(64u, s1 - k);
+    const uint32_t meta = act ? L.meta[kk] : 0u;
+    const int32_t amt = act ? (int32_t)L.amt[kk] : 0;
+    const bool opass = L.oth[kk & (RC_ME - 1)];
+    const uint32_t el = ((meta & RM_EVENT) - c0) & (RC_C - 1);
+    const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
+    const bool check = meta & RM_CHECK;
+    bool ok = act && opass;
+    int32_t eff = 0;
+    if (ok) eff = check ? -amt : ((meta & RM_ADD) ? amt : 0);
+    int32_t pre = wave_incl_scan_i32(eff) - eff;
+    const int64_t B64 = rc_sat_add(A0, D);
+    const int32_t B = B64 > INT32_MAX ? INT32_MAX : (B64 < INT32_MIN ? INT32_MIN : (int32_t)B64);
+    // Failures in lane order: every lane after the last failure found sees the failed amounts so far
+    // added back, so the next failure is the first later candidate with amount - pre > B + acc (a
+    // uniform threshold: one compare, one find-first and one readlane per failure); the failed
+    // amounts are added to the later prefixes once, by a scan, after the last one.
+    const int32_t x = amt - pre;
+    uint64_t q1 = 0;
+    if (RC_PROF) {
+      q1 = clock64();
+      tp[0] += q1 - q0;
+    }
+    const unsigned long long cand = __ballot(ok && check);
+    unsigned long long fails = 0, after = ~0ull;
+    int64_t acc = 0;
+    for (;;) {
+      const int64_t thr = (int64_t)B + acc;
+      if (thr >= INT32_MAX) break;  // no later check can fail
+      const unsigned long long fm = __ballot(x > (int32_t)thr) & cand & after;
+      if (!fm) break;
+      const int jl = __builtin_ctzll(fm);
+      if (RC_PROF) rounds++;
+      acc += __builtin_amdgcn_readlane(amt, jl);
+      fails |= 1ull << jl;
+      after = jl == 63 ? 0ull : ~0ull << (jl + 1);
+    }
+    if (fails) {
+      const bool failed = (fails >> lane) & 1ull;
+      const int32_t fa = failed ? amt : 0;
+      pre += wave_incl_scan_i32(fa) - fa;
+      if (failed) {
+        ok = false;
+        eff = 0;
+      }
+    }
+    if (RC_PROF) tp[1] += clock64() - q1;
+    if (act) {
+      if (check) L.cur[side][el] = amt - pre <= B ? 1 : 0;
+      L.ok[kk] = ok ? 1 : 0;
+      L.dent[kk] = D + pre;
+    }
+    D += __builtin_amdgcn_readlane(pre + eff, (int)n - 1);
+  }
+  if (lane == 0) L.delta[sg] = D;
 }
 
 // Whole-wave walk of segment sg from entry kf (64 entries per step). A check passes iff
@@ -140,20 +307,27 @@ __device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t kf, uint32_t
     int64_t eff = 0;
     if (ok) eff = check ? -amt : ((meta & RM_ADD) ? amt : 0);
     int64_t pre = wave_incl_scan_i64(eff) - eff;
-    // the first failing check fails; take it out and re-test the later lanes; repeat (a failed
-    // debit only raises what later entries see, so each round settles one failure)
-    int floor_lane = -1;
+    // failures in lane order against a uniform threshold (rc_walk_wave32)
+    const int64_t x = amt - (pre + D);
+    const unsigned long long cand = __ballot(ok && check);
+    unsigned long long fails = 0, after = ~0ull;
+    int64_t thr = A0;
     for (;;) {
-      const unsigned long long fm = __ballot(ok && check && lane > floor_lane && amt - (pre + D) > A0);
+      const unsigned long long fm = __ballot(x > thr) & cand & after;
       if (!fm) break;
       const int jl = __builtin_ctzll(fm);
-      const int64_t aj = readlane_i64(amt, jl);
-      if (lane > jl) pre += aj;
-      if (lane == jl) {
+      thr = rc_sat_add(thr, readlane_i64(amt, jl));
+      fails |= 1ull << jl;
+      after = jl == 63 ? 0ull : ~0ull << (jl + 1);
+    }
+    if (fails) {
+      const bool failed = (fails >> lane) & 1ull;
+      const int64_t fa = failed ? amt : 0;
+      pre += wave_incl_scan_i64(fa) - fa;
+      if (failed) {
         ok = false;
         eff = 0;
       }
-      floor_lane = jl;
     }
     if (act) {
       if (check) L.cur[side][el] = amt - (pre + D) <= A0 ? 1 : 0;
@@ -204,33 +378,44 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   if (!g->res_chunked) return;
   const uint32_t t = threadIdx.x;
   const int lane = t & 63;
-  const uint32_t wave = t >> 6;
   const uint32_t nch = (E + RC_C - 1) / RC_C;
   const uint32_t R = g->hot_live;
-  uint64_t prof[4] = {0, 0, 0, 0};  // RC_PROF (thread 0): setup, walks, change detection cycles; walks
+  // RC_PROF (thread 0): setup, walk phase, change detection cycles, sum of the longest wave walk per
+  // iteration; per wave: load+scan and failure-search cycles, failure rounds
+  uint64_t prof[4] = {0, 0, 0, 0};
+  uint64_t wrounds = 0, wt[2] = {0, 0};
   for (uint32_t r = t; r < R; r += RC_T) L.A[r] = rc_clamp(s.rstate[r].A);
   for (uint32_t c = t; c <= nch; c += RC_T) L.cb[c] = s.rc_cb[c];
   __syncthreads();
-  // entries of the next chunk, loaded one chunk ahead (two per thread)
-  uint32_t pm[2] = {0, 0}, pk[2] = {0, 0};
+  // the next chunk's entries and tables, loaded one chunk ahead (two of each per thread)
+  uint32_t pm[2] = {0, 0}, pk[2] = {0, 0}, pe = 0;
   uint64_t pa[2] = {0, 0};
+  uint16_t ps[2] = {0, 0}, pg[2] = {0, 0}, pl[2] = {0, 0};
+  uint4 pc = make_uint4(0, 0, 0, 0);
   auto fetch = [&](uint32_t c) {
     const uint32_t b0 = L.cb[c], b1 = L.cb[c + 1];
+    pc = s.rc_cnt[c];
 #pragma unroll
     for (int j = 0; j < 2; j++) {
-      const uint32_t k = b0 + t + (uint32_t)j * RC_T;
-      if (k < b1) {
-        pm[j] = s.rmeta[k];
-        pk[j] = s.rkey[k];
-        pa[j] = (uint64_t)s.ramt[k];
+      const uint32_t kl = t + (uint32_t)j * RC_T;
+      if (b0 + kl < b1) {
+        pm[j] = s.rmeta[b0 + kl];
+        pk[j] = s.rkey[b0 + kl];
+        pa[j] = (uint64_t)s.ramt[b0 + kl];
+        ps[j] = s.rc_segof[b0 + kl];
+        pl[j] = s.rc_list[b0 + kl];
       }
+      if (b0 + kl <= b1) pg[j] = s.rc_seg[b0 + c + kl];
     }
+    if (c * RC_C + t < E) pe = *(const uint32_t*)&s.rc_ent[2 * (c * RC_C + t)];
   };
   fetch(0);
   uint64_t iters = 0;
   for (uint32_t c = 0; c < nch; c++) {
     const uint32_t cb0 = L.cb[c], m = L.cb[c + 1] - cb0;
     const uint32_t c0 = c * RC_C;
+    const uint32_t nseg = rc_uniform(pc.x), nhuge = rc_uniform(pc.y), nlong = nhuge + rc_uniform(pc.z);
+    const bool big = rc_uniform(pc.w) != 0;
     __syncthreads();  // the previous chunk's LDS is consumed
     const uint64_t tp0 = RC_PROF ? clock64() : 0;
 #pragma unroll
@@ -240,75 +425,37 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
         L.meta[kl] = pm[j];
         L.amt[kl] = pa[j];
         L.rank[kl] = (uint16_t)(pk[j] & RC_RMASK);
+        L.segof[kl] = ps[j];
         L.oth[kl] = 1;
       }
+      if (kl < nseg) {
+        L.lst[kl] = pl[j];
+        L.dfrom[kl] = pg[j];  // every segment is walked in the first iteration
+      }
+      if (kl <= nseg) L.seg[kl] = pg[j];
     }
-    L.ent[0][t] = L.ent[1][t] = RC_NONE;
+    const bool ev = c0 + t < E;
+    L.ent[0][t] = ev ? (uint16_t)pe : (uint16_t)RC_NONE;
+    L.ent[1][t] = ev ? (uint16_t)(pe >> 16) : (uint16_t)RC_NONE;
     L.cur[0][t] = L.cur[1][t] = 1;
     L.prv[0][t] = L.prv[1][t] = 1;
     if (t == 0) {
-      L.nhuge = L.nlong = L.nshort = 0;
+      L.pmax = 0;
       L.qlong = L.qshort = 0;
       L.chg[0] = L.chg[1] = 0;
     }
     if (c + 1 < nch) fetch(c + 1);
     if (m == 0) continue;
     __syncthreads();
-    // segments: ordered compaction of the rank-change positions; each entry's segment id is the
-    // count of starts up to it
-    bool f[2];
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-      const uint32_t kl = t + (uint32_t)j * RC_T;
-      f[j] = kl < m && (kl == 0 || L.rank[kl] != L.rank[kl - 1]);
-      if (kl < m) {
-        const uint32_t meta = L.meta[kl];
-        L.ent[(meta & RM_SIDE) ? 1 : 0][(meta & RM_EVENT) - c0] = (uint16_t)kl;
-      }
-    }
-    const unsigned long long b0 = __ballot(f[0]), b1 = __ballot(f[1]);
-    if (lane == 0) {
-      L.wcnt[0][wave] = (uint32_t)__popcll(b0);
-      L.wcnt[1][wave] = (uint32_t)__popcll(b1);
-    }
-    __syncthreads();
-    uint32_t pre0 = 0, tot0 = 0, pre1 = 0, tot1 = 0;
-    for (uint32_t w = 0; w < RC_T / 64; w++) {
-      const uint32_t a0 = L.wcnt[0][w], a1 = L.wcnt[1][w];
-      pre0 += w < wave ? a0 : 0u;
-      pre1 += w < wave ? a1 : 0u;
-      tot0 += a0;
-      tot1 += a1;
-    }
-    const unsigned long long upto = (2ull << lane) - 1ull;  // lanes <= this one
-    const uint32_t id0 = pre0 + (uint32_t)__popcll(b0 & upto) - 1u;
-    const uint32_t id1 = tot0 + pre1 + (uint32_t)__popcll(b1 & upto) - 1u;
-    if (f[0]) L.seg[id0] = (uint16_t)t;
-    if (f[1]) L.seg[id1] = (uint16_t)(t + RC_T);
-    if (t < m) L.segof[t] = (uint16_t)id0;
-    if (t + RC_T < m) L.segof[t + RC_T] = (uint16_t)id1;
-    const uint32_t nseg = tot0 + tot1;
-    if (t == 0) {
-      L.seg[nseg] = (uint16_t)m;
-      L.nseg = nseg;
-    }
-    __syncthreads();
-    for (uint32_t sg = t; sg < nseg; sg += RC_T) {
-      const uint32_t len = (uint32_t)(L.seg[sg + 1] - L.seg[sg]);
-      L.dfrom[sg] = L.seg[sg];  // every segment is walked in the first iteration
-      if (len > 64) L.lng[atomicAdd(&L.nhuge, 1u)] = (uint16_t)sg;
-      else if (len > RC_LONG) L.lng[RC_ME - 1u - atomicAdd(&L.nlong, 1u)] = (uint16_t)sg;
-      else L.sht[atomicAdd(&L.nshort, 1u)] = (uint16_t)sg;
-    }
-    __syncthreads();
     RC_ADD(0, tp0);
-    const uint32_t nhuge = rc_uniform(L.nhuge), nlong = nhuge + rc_uniform(L.nlong), nshort = rc_uniform(L.nshort);
+    const uint32_t nshort = nseg - nlong;
     for (uint32_t it = 0;; it++) {
       if (it > RC_C + 1) {  // cannot happen (see header); the sequential walker takes the window
         if (t == 0) g->res_error = 1;
         return;
       }
       const uint64_t tw0 = RC_PROF ? clock64() : 0;
+      uint64_t busy = 0;
       // the dirty segments, from their first changed entry: long ones one per wave (the longest
       // first), short ones one per lane. Every lane of the wave adds 1 (one LDS atomic of 64 after the
       // compiler's wave aggregation): the long queue counts 64 per grab, the short queue hands each
@@ -317,18 +464,22 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
       for (;;) {
         const uint32_t j = rc_uniform(atomicAdd(&L.qlong, 1u)) >> 6;
         if (j >= nlong) break;
-        const uint32_t sg = rc_uniform(j < nhuge ? L.lng[j] : L.lng[RC_ME - 1u - (j - nhuge)]);
+        const uint32_t sg = rc_uniform(L.lst[j]);
         const uint32_t kf = rc_uniform(L.dfrom[sg]);
         if (kf == RC_NONE) continue;
         L.dfrom[sg] = RC_NONE;
-        rc_walk_wave(L, sg, kf, c0, lane);
-        if (RC_PROF && t == 0) prof[3]++;
+        const uint64_t tb0 = RC_PROF ? clock64() : 0;
+        if (big) rc_walk_wave(L, sg, kf, c0, lane);
+        else rc_walk_wave32(L, sg, kf, c0, lane, wrounds, wt);
+        if (RC_PROF) {
+          busy += clock64() - tb0;
+        }
       }
       for (;;) {
         const uint32_t j = atomicAdd(&L.qshort, 1u);
         if (rc_uniform(j) >= nshort) break;
         if (j < nshort) {
-          const uint32_t sg = L.sht[j];
+          const uint32_t sg = L.lst[nlong + j];
           const uint32_t kf = L.dfrom[sg];
           if (kf != RC_NONE) {
             L.dfrom[sg] = RC_NONE;
@@ -336,8 +487,13 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
           }
         }
       }
+      if (RC_PROF && lane == 0) atomicMax(&L.pmax, (uint32_t)busy);
       __syncthreads();
       RC_ADD(1, tw0);
+      if (RC_PROF && t == 0) {
+        prof[3] += L.pmax;
+        L.pmax = 0;
+      }
       const uint64_t td0 = RC_PROF ? clock64() : 0;
       // changed checks mark their readers' segments dirty from the reading entry
       if (t == 0) {
@@ -375,6 +531,11 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
       const uint32_t kl = t + (uint32_t)j * RC_T;
       if (kl < m) s.rown[cb0 + kl] = L.ok[kl];
     }
+  }
+  if (RC_PROF) {
+    if (lane == 0) atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)wt[0]);
+    if (lane == 0) atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)wt[1]);
+    if (lane == 0) atomicAdd((unsigned long long*)&g->dbg[1], (unsigned long long)wrounds);
   }
   if (t == 0) {
     g->dbg[0] += iters;

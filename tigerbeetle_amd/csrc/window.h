@@ -109,7 +109,12 @@ struct Scratch {
   // (debits of a debits<=credits account, credits of a credits<=debits one; bit 63 = must stay hot)
   uint32_t* bind_slot;
   unsigned long long* bind_adv;
-  uint32_t* rc_cb;  // chunked resolver (chunks.h): first sorted entry of each 1024-event chunk
+  // chunked resolver (chunks.h): first sorted entry of each 1024-event chunk, and the per-chunk
+  // tables k_rc_prep builds (segment of each entry, segment starts, walk lists, entry of each event
+  // side, counts)
+  uint32_t* rc_cb;
+  uint16_t *rc_segof, *rc_seg, *rc_list, *rc_ent;
+  uint4* rc_cnt;
   // pulse_next (k_pn): per event the op's value (C_PNOP) and, for a walker post/void of a pending
   // transfer created in the window, that transfer's event index; per segment the min creation value
   // and the count of resets among the events that ran ok
