@@ -184,13 +184,15 @@ __global__ void __launch_bounds__(RC_T) k_rc_prep(Dev d, Scratch s, uint32_t E) 
   if (t == 0) s.rc_cnt[c] = make_uint4(nseg, nh, nl, big);
 }
 
-// A is kept clamped into int64: every decision compares amount - (pre + D) with it, where amount and
-// |pre + D| (a segment's effects, bounded by the window's amounts) are below 2^62, so a clamped value
-// decides exactly as the exact one; and A + delta of a clamped A stays beyond +-2^62, on the same side
-// of every comparison (the exact balances are applied by k_res_sum / k_res_apply, not from A).
+// A is the pre-window balance clamped into [-2^62, 2^62] plus the window's effects so far: a check
+// fails iff amount > A_exact + P, where P sums effects of other events of the window, and amount + |P|
+// is below the window's amount sum < 2^62. So A_exact >= 2^62 never fails and A_exact <= -2^62
+// always fails, exactly as the clamped value decides, and A never leaves int64 (the exact balances
+// are applied by k_res_sum / k_res_apply, not from A).
 __device__ inline int64_t rc_clamp(__int128 a) {
-  if (a > (__int128)INT64_MAX) return INT64_MAX;
-  if (a < (__int128)INT64_MIN) return INT64_MIN;
+  const __int128 lim = (__int128)1 << 62;
+  if (a > lim) return (int64_t)lim;
+  if (a < -lim) return -(int64_t)lim;
   return (int64_t)a;
 }
 __device__ inline int64_t rc_sat_add(int64_t a, int64_t b) {
@@ -224,14 +226,26 @@ __device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, uint32
   const uint32_t s1 = rc_uniform(L.seg[sg + 1]);
   const int64_t A0 = rc_uniform64(L.A[L.rank[kf]]);
   int64_t D = rc_uniform64(kf == rc_uniform(L.seg[sg]) ? 0 : L.dent[kf]);
+  // the step's LDS inputs are loaded one step ahead (no step's stores touch them)
+  uint32_t kk = kf + (uint32_t)lane;
+  // (kept raw until used: converting a prefetched value at once would wait for its load)
+  uint32_t meta_n = kk < s1 ? L.meta[kk] : 0u;
+  int32_t amt_n = kk < s1 ? (int32_t)L.amt[kk] : 0;
+  uint32_t oth_n = L.oth[kk & (RC_ME - 1)];
   for (uint32_t k = kf; k < s1; k += 64) {
     const uint64_t q0 = RC_PROF ? clock64() : 0;
-    const uint32_t kk = k + (uint32_t)lane;
+    kk = k + (uint32_t)lane;
     const bool act = kk < s1;
     const uint32_t n = min(64u, s1 - k);
-    const uint32_t meta = act ? L.meta[kk] : 0u;
-    const int32_t amt = act ? (int32_t)L.amt[kk] : 0;
-    const bool opass = L.oth[kk & (RC_ME - 1)];
+    const uint32_t meta = meta_n;
+    const int32_t amt = amt_n;
+    const bool opass = oth_n != 0u;
+    if (k + 64u < s1) {
+      const uint32_t kn = kk + 64u;
+      meta_n = kn < s1 ? L.meta[kn] : 0u;
+      amt_n = kn < s1 ? (int32_t)L.amt[kn] : 0;
+      oth_n = L.oth[kn & (RC_ME - 1)];
+    }
     const uint32_t el = ((meta & RM_EVENT) - c0) & (RC_C - 1);
     const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
     const bool check = meta & RM_CHECK;
@@ -239,8 +253,11 @@ __device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, uint32
     int32_t eff = 0;
     if (ok) eff = check ? -amt : ((meta & RM_ADD) ? amt : 0);
     int32_t pre = wave_incl_scan_i32(eff) - eff;
-    const int64_t B64 = rc_sat_add(A0, D);
-    const int32_t B = B64 > INT32_MAX ? INT32_MAX : (B64 < INT32_MIN ? INT32_MIN : (int32_t)B64);
+    // B = A0 + D clamped into int32 with 32-bit scalar operations (|A0| <= 2^62, |D| < 2^62)
+    const int64_t B64 = A0 + D;
+    const uint32_t blo = (uint32_t)B64;
+    const int32_t bhi = (int32_t)(B64 >> 32);
+    const int32_t B = bhi == ((int32_t)blo >> 31) ? (int32_t)blo : (bhi < 0 ? INT32_MIN : INT32_MAX);
     // Failures in lane order: every lane after the last failure found sees the failed amounts so far
     // added back, so the next failure is the first later candidate with amount - pre > B + acc (a
     // uniform threshold: one compare, one find-first and one readlane per failure); the failed
@@ -253,15 +270,14 @@ __device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, uint32
     }
     const unsigned long long cand = __ballot(ok && check);
     unsigned long long fails = 0, after = ~0ull;
-    int64_t acc = 0;
-    for (;;) {
-      const int64_t thr = (int64_t)B + acc;
-      if (thr >= INT32_MAX) break;  // no later check can fail
-      const unsigned long long fm = __ballot(x > (int32_t)thr) & cand & after;
+    const uint32_t room = (uint32_t)INT32_MAX - (uint32_t)B;  // B + acc stays an int32 below it
+    uint32_t acc = 0;
+    while (acc < room) {
+      const unsigned long long fm = __ballot(x > B + (int32_t)acc) & cand & after;
       if (!fm) break;
       const int jl = __builtin_ctzll(fm);
       if (RC_PROF) rounds++;
-      acc += __builtin_amdgcn_readlane(amt, jl);
+      acc += (uint32_t)__builtin_amdgcn_readlane(amt, jl);
       fails |= 1ull << jl;
       after = jl == 63 ? 0ull : ~0ull << (jl + 1);
     }
@@ -469,8 +485,12 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
         if (kf == RC_NONE) continue;
         L.dfrom[sg] = RC_NONE;
         const uint64_t tb0 = RC_PROF ? clock64() : 0;
+        // the longest walks (the Zipf head's) are the iteration's critical path: they issue first
+        // on their SIMD while other waves walk short segments beside them
+        if (j < nhuge) __builtin_amdgcn_s_setprio(3);
         if (big) rc_walk_wave(L, sg, kf, c0, lane);
         else rc_walk_wave32(L, sg, kf, c0, lane, wrounds, wt);
+        __builtin_amdgcn_s_setprio(0);
         if (RC_PROF) {
           busy += clock64() - tb0;
         }
@@ -523,7 +543,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
     // the chunk is final: advance A, publish the statuses and the committed entries
     for (uint32_t sg = t; sg < nseg; sg += RC_T) {
       const uint32_t r = L.rank[L.seg[sg]];
-      L.A[r] = rc_sat_add(L.A[r], L.delta[sg]);
+      L.A[r] += L.delta[sg];
     }
     if (c0 + t < E) s.st[c0 + t] = (L.cur[0][t] ? ST_DR_PASS : 0u) | (L.cur[1][t] ? ST_CR_PASS : 0u);
 #pragma unroll

@@ -130,7 +130,7 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t res_chunked;
   uint64_t res_chunk_windows;  // cumulative windows the chunked resolver decided
   uint32_t cpw_want;  // last window: W events in a window the component walkers could take (host readback)
-  uint32_t pad5;
+  uint32_t rc_last;   // last window: the chunked resolver decided it (host readback, read with cpw_want)
 };
 
 // Whether this block is the last of its grid to arrive (every thread of every block calls it once).

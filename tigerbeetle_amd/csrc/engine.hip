@@ -1309,6 +1309,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     gw->windows_applied++;
     gw->hot_count = 0;
     gw->hot_live = 0;
+    gw->rc_last = gw->res_chunked;
     gw->res_chunked = 0;
     gw->res_inelig = 0;
     gw->res_error = 0;

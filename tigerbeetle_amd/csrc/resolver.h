@@ -94,10 +94,11 @@ __device__ inline bool rc_eligible(const Globals* g, uint32_t E) {
 
 // Keys: one (hot rank, 2*event+side) pair per side of a W event (not failed in validation) whose
 // account is hot. Also zeroes the per-event status words and the per-rank segments.
-__global__ void __launch_bounds__(256) k_res_keys(Dev d, Scratch s, uint32_t E, uint32_t epoch, uint32_t allow_chunks) {
+__global__ void __launch_bounds__(256) k_res_keys(Dev d, Scratch s, uint32_t E, uint32_t epoch, uint32_t allow_chunks,
+                                                  uint32_t allow_relax) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   Globals* g = d.g;
-  const bool active = !g->res_inelig && g->hot_count;
+  bool active = !g->res_inelig && g->hot_count;
   if (active && i < g->hot_count) {
     s.rstate[i].start = 0;
     s.rstate[i].end = 0;
@@ -110,6 +111,12 @@ __global__ void __launch_bounds__(256) k_res_keys(Dev d, Scratch s, uint32_t E, 
   // chunked mode (chunks.h): keys (1024-event chunk, compact rank), else (rank)
   const bool chunked = active && allow_chunks && rc_eligible(g, E);
   if (i == 0) g->res_chunked = chunked ? 1u : 0u;
+  if (active && !chunked && !allow_relax) {
+    // the host did not launch the relaxation (it predicted a chunked window): the sequential walker
+    // decides this window; the host's next prediction comes from this window
+    if (i == 0) g->res_inelig = 1;
+    active = false;
+  }
   if (i >= E) return;
   s.kidx[2 * i] = NONE32;
   s.kidx[2 * i + 1] = NONE32;
