@@ -87,6 +87,7 @@ def _run(resolver, seed, n_acc, win, bm, n_windows, pending_pct, zipf_s, amount_
     (3, 2000, 16, 8190, 10, 1.1, 5000), # many accounts, long hot lists (multi-step walks)
     (4, 20, 2, 8190, 50, 0.5, 50),      # few accounts, everything hot, near-uniform
     (5, 100, 4, 2048, 20, 1.2, 1 << 61), # window amount sums above 2^62: 128-bit walker steps
+    (6, 100, 4, 2048, 20, 1.2, 1 << 36), # amounts >= 2^24: chunked resolver's int64 wave walks
 ])
 def test_resolver_matches_oracle_and_walker(seed, n_acc, win, bm, pending_pct, zipf_s, amount_max, monkeypatch):
     rep_r, st_r = _run("relax", seed, n_acc, win, bm, 6, pending_pct, zipf_s, amount_max)
