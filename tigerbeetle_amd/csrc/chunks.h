@@ -28,6 +28,11 @@
 #define RC_T 1024  // threads of the workgroup
 #define RC_ME (2 * RC_C)  // entries per chunk at most
 #define RC_LONG 8  // longer segments are walked by a whole wave
+// Entry encoding in LDS (k_rc_prep): bits 0-10 the (side, event) check slot (side << 10 | event in
+// chunk), bit 11 the entry's side checks (a limit), bit 12 a committed entry raises A.
+#define RC_EM_IDX 0x7FFu
+#define RC_EM_CHECK 0x800u
+#define RC_EM_ADD 0x1000u
 #ifndef RC_PROF
 #define RC_PROF 0  // 1: per-phase clock64() sums of k_rc_run into Globals::dbg (tbg_debug_counters)
 #endif
@@ -89,16 +94,15 @@ struct RcLds {
   uint64_t amt[RC_ME];         // the chunk's entries, grouped by rank, event order inside a rank
   int64_t dent[RC_ME];         // per entry: the segment's effects on A before it (last walk)
   int64_t delta[RC_ME];        // per segment: its effects on A (last walk)
-  uint32_t meta[RC_ME];
+  uint16_t em[RC_ME];          // entry encoding (RC_EM_*)
   uint32_t dfrom[RC_ME];       // per segment: first entry whose input changed (RC_NONE: clean)
   uint16_t rank[RC_ME];
   uint16_t segof[RC_ME];       // entry -> segment
   uint16_t seg[RC_ME + 1];     // segment starts (entry index), seg[nseg] = entries
   uint16_t lst[RC_ME];         // segment ids: long ones (the longest first), then short ones
   uint16_t ent[2][RC_C];       // per side and event: its entry (RC_NONE: that side is not hot)
-  uint8_t ok[RC_ME];           // entry's effect applies (the event commits)
   uint8_t oth[RC_ME];          // per entry: the other side's check as its reader sees it (1 = pass)
-  uint8_t cur[2][RC_C], prv[2][RC_C];  // per side: latest check / the one readers use (1 = pass)
+  uint8_t cur[2 * RC_C], prv[2][RC_C];  // per (side, event): latest check / the one readers use (1 = pass)
   uint32_t cb[1024 + 1];        // first entry of every chunk (no global load on a chunk's critical path)
   uint32_t qlong, qshort, chg[2];
   uint32_t pmax;  // RC_PROF: longest wave walk of the iteration (cycles)
@@ -135,7 +139,10 @@ __global__ void __launch_bounds__(RC_T) k_rc_prep(Dev d, Scratch s, uint32_t E) 
     f[j] = kl < m && (kl == 0 || rank[kl] != rank[kl - 1]);
     if (kl < m) {
       const uint32_t meta = s.rmeta[cb0 + kl];
-      s.rc_ent[2 * (meta & RM_EVENT) + ((meta & RM_SIDE) ? 1 : 0)] = (uint16_t)kl;
+      const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
+      s.rc_ent[2 * (meta & RM_EVENT) + side] = (uint16_t)kl;
+      s.rc_em[cb0 + kl] = (uint16_t)((side << 10) | ((meta & RM_EVENT) - c0) | ((meta & RM_CHECK) ? RC_EM_CHECK : 0u) |
+                                     ((meta & RM_ADD) ? RC_EM_ADD : 0u));
     }
   }
   const unsigned long long b0 = __ballot(f[0]), b1 = __ballot(f[1]);
@@ -221,15 +228,17 @@ __device__ inline int32_t wave_incl_scan_i32(int32_t x) {
 // in-step prefix and amount - prefix fit an int32 (|.| < 65 * 2^24), and a check fails iff
 // amount - pre > A0 + D, with A0 + D clamped into int32 without changing any comparison. Same
 // outputs as rc_walk_wave.
-__device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, uint32_t c0, int lane, uint64_t& rounds,
+
+__device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, int lane, uint64_t& rounds,
                                       uint64_t* tp) {
-  const uint32_t s1 = rc_uniform(L.seg[sg + 1]);
-  const int64_t A0 = rc_uniform64(L.A[L.rank[kf]]);
-  int64_t D = rc_uniform64(kf == rc_uniform(L.seg[sg]) ? 0 : L.dent[kf]);
-  // the step's LDS inputs are loaded one step ahead (no step's stores touch them)
+  const uint32_t s0 = rc_uniform(L.seg[sg]), s1 = rc_uniform(L.seg[sg + 1]);
+  const int64_t A0 = rc_uniform64(L.A[L.rank[s0]]);
+  // a re-walk starts at the first entry whose input changed, from the balance kept before it
+  int64_t D = kf == s0 ? 0 : rc_uniform64(L.dent[kf]);
+  // the step's LDS inputs are loaded one step ahead (no step's stores touch them), kept raw until
+  // used (converting a prefetched value at once would wait for its load)
   uint32_t kk = kf + (uint32_t)lane;
-  // (kept raw until used: converting a prefetched value at once would wait for its load)
-  uint32_t meta_n = kk < s1 ? L.meta[kk] : 0u;
+  uint32_t em_n = kk < s1 ? L.em[kk] : 0u;
   int32_t amt_n = kk < s1 ? (int32_t)L.amt[kk] : 0;
   uint32_t oth_n = L.oth[kk & (RC_ME - 1)];
   for (uint32_t k = kf; k < s1; k += 64) {
@@ -237,21 +246,19 @@ __device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, uint32
     kk = k + (uint32_t)lane;
     const bool act = kk < s1;
     const uint32_t n = min(64u, s1 - k);
-    const uint32_t meta = meta_n;
+    const uint32_t em = em_n;
     const int32_t amt = amt_n;
     const bool opass = oth_n != 0u;
     if (k + 64u < s1) {
       const uint32_t kn = kk + 64u;
-      meta_n = kn < s1 ? L.meta[kn] : 0u;
+      em_n = kn < s1 ? L.em[kn] : 0u;
       amt_n = kn < s1 ? (int32_t)L.amt[kn] : 0;
       oth_n = L.oth[kn & (RC_ME - 1)];
     }
-    const uint32_t el = ((meta & RM_EVENT) - c0) & (RC_C - 1);
-    const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
-    const bool check = meta & RM_CHECK;
+    const bool check = em & RC_EM_CHECK;
     bool ok = act && opass;
     int32_t eff = 0;
-    if (ok) eff = check ? -amt : ((meta & RM_ADD) ? amt : 0);
+    if (ok) eff = check ? -amt : ((em & RC_EM_ADD) ? amt : 0);
     int32_t pre = wave_incl_scan_i32(eff) - eff;
     // B = A0 + D clamped into int32 with 32-bit scalar operations (|A0| <= 2^62, |D| < 2^62)
     const int64_t B64 = A0 + D;
@@ -285,15 +292,11 @@ __device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, uint32
       const bool failed = (fails >> lane) & 1ull;
       const int32_t fa = failed ? amt : 0;
       pre += wave_incl_scan_i32(fa) - fa;
-      if (failed) {
-        ok = false;
-        eff = 0;
-      }
+      if (failed) eff = 0;
     }
     if (RC_PROF) tp[1] += clock64() - q1;
     if (act) {
-      if (check) L.cur[side][el] = amt - pre <= B ? 1 : 0;
-      L.ok[kk] = ok ? 1 : 0;
+      if (check) L.cur[em & RC_EM_IDX] = amt - pre <= B ? 1 : 0;
       L.dent[kk] = D + pre;
     }
     D += __builtin_amdgcn_readlane(pre + eff, (int)n - 1);
@@ -301,27 +304,24 @@ __device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, uint32
   if (lane == 0) L.delta[sg] = D;
 }
 
-// Whole-wave walk of segment sg from entry kf (64 entries per step). A check passes iff
-// amount <= A0 + D + pre, i.e. amount - (pre + D) <= A0. Re-walks start at the first entry whose
-// input changed, from the D recorded before it by the previous walk.
-__device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t kf, uint32_t c0, int lane) {
+// Whole-wave walk of segment sg (64 entries per step), any amounts below 2^62. A check passes iff
+// amount <= A0 + D + pre, i.e. amount - (pre + D) <= A0.
+__device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t kf, int lane) {
   // wave-uniform bounds (SGPRs): the step loop and its ballots are uniform control flow
-  const uint32_t s1 = rc_uniform(L.seg[sg + 1]);
-  const int64_t A0 = rc_uniform64(L.A[L.rank[kf]]);
-  int64_t D = rc_uniform64(kf == rc_uniform(L.seg[sg]) ? 0 : L.dent[kf]);
+  const uint32_t s0 = rc_uniform(L.seg[sg]), s1 = rc_uniform(L.seg[sg + 1]);
+  const int64_t A0 = rc_uniform64(L.A[L.rank[s0]]);
+  int64_t D = kf == s0 ? 0 : rc_uniform64(L.dent[kf]);
   for (uint32_t k = kf; k < s1; k += 64) {
     const uint32_t kk = k + (uint32_t)lane;
     const bool act = kk < s1;
     const uint32_t n = min(64u, s1 - k);
-    const uint32_t meta = act ? L.meta[kk] : 0u;
+    const uint32_t em = act ? L.em[kk] : 0u;
     const int64_t amt = act ? (int64_t)L.amt[kk] : 0;
-    const uint32_t el = ((meta & RM_EVENT) - c0) & (RC_C - 1);
-    const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
-    const bool check = meta & RM_CHECK;
+    const bool check = em & RC_EM_CHECK;
     const bool opass = L.oth[kk & (RC_ME - 1)];  // 1 unless the other side's check failed
     bool ok = act && opass;
     int64_t eff = 0;
-    if (ok) eff = check ? -amt : ((meta & RM_ADD) ? amt : 0);
+    if (ok) eff = check ? -amt : ((em & RC_EM_ADD) ? amt : 0);
     int64_t pre = wave_incl_scan_i64(eff) - eff;
     // failures in lane order against a uniform threshold (rc_walk_wave32)
     const int64_t x = amt - (pre + D);
@@ -332,7 +332,7 @@ __device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t kf, uint32_t
       const unsigned long long fm = __ballot(x > thr) & cand & after;
       if (!fm) break;
       const int jl = __builtin_ctzll(fm);
-      thr = rc_sat_add(thr, readlane_i64(amt, jl));
+      thr += readlane_i64(amt, jl);
       fails |= 1ull << jl;
       after = jl == 63 ? 0ull : ~0ull << (jl + 1);
     }
@@ -340,14 +340,10 @@ __device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t kf, uint32_t
       const bool failed = (fails >> lane) & 1ull;
       const int64_t fa = failed ? amt : 0;
       pre += wave_incl_scan_i64(fa) - fa;
-      if (failed) {
-        ok = false;
-        eff = 0;
-      }
+      if (failed) eff = 0;
     }
     if (act) {
-      if (check) L.cur[side][el] = amt - (pre + D) <= A0 ? 1 : 0;
-      L.ok[kk] = ok ? 1 : 0;
+      if (check) L.cur[em & RC_EM_IDX] = amt - (pre + D) <= A0 ? 1 : 0;
       L.dent[kk] = D + pre;
     }
     D += readlane_i64(pre + eff, (int)n - 1);
@@ -355,29 +351,23 @@ __device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t kf, uint32_t
   if (lane == 0) L.delta[sg] = D;
 }
 
-// One lane walks segment sg from entry kf.
-__device__ inline void rc_walk_lane(RcLds& L, uint32_t sg, uint32_t kf, uint32_t c0) {
-  const uint32_t s1 = L.seg[sg + 1];
-  const int64_t A0 = L.A[L.rank[kf]];
-  int64_t D = kf == L.seg[sg] ? 0 : L.dent[kf];
-  for (uint32_t k = kf; k < s1; k++) {
-    const uint32_t meta = L.meta[k];
+// One lane walks a short segment (at most RC_LONG entries, always from its start: dirty marks of
+// short segments are only consumed as "walk it").
+__device__ inline void rc_walk_lane(RcLds& L, uint32_t sg) {
+  const uint32_t s0 = L.seg[sg], s1 = L.seg[sg + 1];
+  const int64_t A0 = L.A[L.rank[s0]];
+  int64_t D = 0;
+  for (uint32_t k = s0; k < s1; k++) {
+    const uint32_t em = L.em[k];
     const int64_t amt = (int64_t)L.amt[k];
-    const uint32_t el = ((meta & RM_EVENT) - c0) & (RC_C - 1);
-    const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
     const bool opass = L.oth[k];
-    L.dent[k] = D;
-    bool ok;
-    if (meta & RM_CHECK) {
+    if (em & RC_EM_CHECK) {
       const bool pass = amt - D <= A0;
-      L.cur[side][el] = pass ? 1 : 0;
-      ok = opass && pass;
-      if (ok) D -= amt;
-    } else {
-      ok = opass;
-      if (ok && (meta & RM_ADD)) D += amt;
+      L.cur[em & RC_EM_IDX] = pass ? 1 : 0;
+      if (opass && pass) D -= amt;
+    } else if (opass && (em & RC_EM_ADD)) {
+      D += amt;
     }
-    L.ok[k] = ok ? 1 : 0;
   }
   L.delta[sg] = D;
 }
@@ -399,12 +389,13 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   // RC_PROF (thread 0): setup, walk phase, change detection cycles, sum of the longest wave walk per
   // iteration; per wave: load+scan and failure-search cycles, failure rounds
   uint64_t prof[4] = {0, 0, 0, 0};
-  uint64_t wrounds = 0, wt[2] = {0, 0};
+  uint64_t wrounds = 0, wt[2] = {0, 0}, hz[4] = {0, 0, 0, 0};  // RC_PROF: huge walks (cycles, steps) it 0 / later
   for (uint32_t r = t; r < R; r += RC_T) L.A[r] = rc_clamp(s.rstate[r].A);
   for (uint32_t c = t; c <= nch; c += RC_T) L.cb[c] = s.rc_cb[c];
   __syncthreads();
   // the next chunk's entries and tables, loaded one chunk ahead (two of each per thread)
-  uint32_t pm[2] = {0, 0}, pk[2] = {0, 0}, pe = 0;
+  uint32_t pk[2] = {0, 0}, pe = 0;
+  uint16_t pm[2] = {0, 0};
   uint64_t pa[2] = {0, 0};
   uint16_t ps[2] = {0, 0}, pg[2] = {0, 0}, pl[2] = {0, 0};
   uint4 pc = make_uint4(0, 0, 0, 0);
@@ -415,7 +406,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
     for (int j = 0; j < 2; j++) {
       const uint32_t kl = t + (uint32_t)j * RC_T;
       if (b0 + kl < b1) {
-        pm[j] = s.rmeta[b0 + kl];
+        pm[j] = s.rc_em[b0 + kl];
         pk[j] = s.rkey[b0 + kl];
         pa[j] = (uint64_t)s.ramt[b0 + kl];
         ps[j] = s.rc_segof[b0 + kl];
@@ -438,7 +429,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
     for (int j = 0; j < 2; j++) {
       const uint32_t kl = t + (uint32_t)j * RC_T;
       if (kl < m) {
-        L.meta[kl] = pm[j];
+        L.em[kl] = pm[j];
         L.amt[kl] = pa[j];
         L.rank[kl] = (uint16_t)(pk[j] & RC_RMASK);
         L.segof[kl] = ps[j];
@@ -453,7 +444,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
     const bool ev = c0 + t < E;
     L.ent[0][t] = ev ? (uint16_t)pe : (uint16_t)RC_NONE;
     L.ent[1][t] = ev ? (uint16_t)(pe >> 16) : (uint16_t)RC_NONE;
-    L.cur[0][t] = L.cur[1][t] = 1;
+    L.cur[t] = L.cur[RC_C + t] = 1;
     L.prv[0][t] = L.prv[1][t] = 1;
     if (t == 0) {
       L.pmax = 0;
@@ -488,11 +479,16 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
         // the longest walks (the Zipf head's) are the iteration's critical path: they issue first
         // on their SIMD while other waves walk short segments beside them
         if (j < nhuge) __builtin_amdgcn_s_setprio(3);
-        if (big) rc_walk_wave(L, sg, kf, c0, lane);
-        else rc_walk_wave32(L, sg, kf, c0, lane, wrounds, wt);
+        if (big) rc_walk_wave(L, sg, kf, lane);
+        else rc_walk_wave32(L, sg, kf, lane, wrounds, wt);
         __builtin_amdgcn_s_setprio(0);
         if (RC_PROF) {
-          busy += clock64() - tb0;
+          const uint64_t dt = clock64() - tb0;
+          busy += dt;
+          if (j < nhuge) {
+            hz[it == 0 ? 0 : 2] += dt;
+            hz[it == 0 ? 1 : 3] += (rc_uniform(L.seg[sg + 1]) - kf + 63) / 64;
+          }
         }
       }
       for (;;) {
@@ -503,7 +499,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
           const uint32_t kf = L.dfrom[sg];
           if (kf != RC_NONE) {
             L.dfrom[sg] = RC_NONE;
-            rc_walk_lane(L, sg, kf, c0);
+            rc_walk_lane(L, sg);
           }
         }
       }
@@ -523,7 +519,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
       bool ch = false;
 #pragma unroll
       for (int sd = 0; sd < 2; sd++) {
-        const uint8_t v = L.cur[sd][t];
+        const uint8_t v = L.cur[sd * RC_C + t];
         if (v != L.prv[sd][t]) {
           L.prv[sd][t] = v;
           const uint32_t r = L.ent[sd ^ 1][t];
@@ -545,21 +541,31 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
       const uint32_t r = L.rank[L.seg[sg]];
       L.A[r] += L.delta[sg];
     }
-    if (c0 + t < E) s.st[c0 + t] = (L.cur[0][t] ? ST_DR_PASS : 0u) | (L.cur[1][t] ? ST_CR_PASS : 0u);
+    if (c0 + t < E) s.st[c0 + t] = (L.cur[t] ? ST_DR_PASS : 0u) | (L.cur[RC_C + t] ? ST_CR_PASS : 0u);
+    // an entry's effect applies iff the other side's check passed and its own (if it checks) did
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       const uint32_t kl = t + (uint32_t)j * RC_T;
-      if (kl < m) s.rown[cb0 + kl] = L.ok[kl];
+      if (kl < m) {
+        const uint32_t em = L.em[kl];
+        s.rown[cb0 + kl] = (L.oth[kl] && (!(em & RC_EM_CHECK) || L.cur[em & RC_EM_IDX])) ? 1u : 0u;
+      }
     }
   }
   if (RC_PROF) {
-    if (lane == 0) atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)wt[0]);
+    if (RC_PROF == 1 && lane == 0) atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)wt[0]);
     if (lane == 0) atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)wt[1]);
     if (lane == 0) atomicAdd((unsigned long long*)&g->dbg[1], (unsigned long long)wrounds);
+    if (RC_PROF > 1 && lane == 0) {  // huge-walk split instead of setup / detect / pmax
+      atomicAdd((unsigned long long*)&g->dbg[2], (unsigned long long)hz[0]);
+      atomicAdd((unsigned long long*)&g->dbg[4], (unsigned long long)hz[1]);
+      atomicAdd((unsigned long long*)&g->dbg[5], (unsigned long long)hz[2]);
+      atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)hz[3]);
+    }
   }
   if (t == 0) {
     g->dbg[0] += iters;
-    if (RC_PROF)
+    if (RC_PROF == 1)
       for (int k = 0; k < 4; k++) g->dbg[2 + k] += prof[k];
     g->res_chunk_windows++;
   }
