@@ -13,7 +13,6 @@
 //                       W = U + events touching a hot account, closed over linked chains
 //                       (one thread per chain head); all other events get their final outcome here,
 //                       including whole static chains (first failure + linked_event_failed fill).
-//   k_wcount     grid   per-segment counts (W, failures, inserts).
 //   k_wlist      grid   ordered W list (segment prefix + block scan).
 //   k_walk       1 WG   the sequential walker over W only (walker.h).
 //   k_final      grid   ordered per-batch replies, insert ranks, inserts (records appended in
@@ -402,6 +401,11 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     }
     if (cls & C_HIST) atomicOr(&aux, 32u);
     if (cls & C_REACH) atomicMax(&id_max, (unsigned long long)x_id_key(t.id));
+    if ((i & (SEG - 1)) == 0) {  // the segment counts k_classify accumulates
+      s.cnt_w[i / SEG] = 0;
+      s.cnt_bad[i / SEG] = 0;
+      s.cnt_ins[i / SEG] = 0;
+    }
     prec = (cls & C_PREP_REC) != 0;
     // Hot marks: the first marker of an account this window gives it the next dense rank.
     if (cls & C_READS_DR) mark_hot(d, s, dr_slot, epoch);
@@ -538,6 +542,11 @@ __global__ void __launch_bounds__(256) k_ca_prep(Dev d, Scratch s, const tb_acco
   if (i >= w.E || WIN_REJECTED(d.g)) return;
   const tb_account_t a = ev[i];
   const uint32_t b = win_batch(w, i);
+  if ((i & (SEG - 1)) == 0) {  // the segment counts k_classify accumulates
+    s.cnt_w[i / SEG] = 0;
+    s.cnt_bad[i / SEG] = 0;
+    s.cnt_ins[i / SEG] = 0;
+  }
   uint32_t cls = 0, code, id_ent = NONE32, slot = NONE32;
   if (a.flags & TB_ACCOUNT_LINKED) cls |= C_LINKED;
   if (a.timestamp != 0) {
@@ -626,9 +635,29 @@ __device__ inline uint32_t id_alone_bit(const Scratch& s, uint32_t j, uint32_t c
   return (claim_free || bmap_idc(s.bmap, s.id_ent[j], epoch) == 1) ? C_IDALONE : 0u;
 }
 
+// Segment counts (W events; failures and inserts of the others), kept by the thread that decides
+// each event: its block's segment in `packed` (11-bit fields: W | bad << 11 | inserted << 22, at most
+// SEG each), another segment's (a chain running past the segment end) by global atomics. The
+// counters were zeroed by the window's prep kernel.
+struct SegTally {
+  uint32_t seg, packed;
+  __device__ void add(const Scratch& s, uint32_t j, uint32_t cls, uint32_t code) {
+    const bool w = cls & C_W;
+    const uint32_t v = w ? 1u : (((code != TB_CT_OK) ? 1u << 11 : 0u) | ((cls & C_INSERTED) ? 1u << 22 : 0u));
+    const uint32_t sg = j / SEG;
+    if (sg == seg) {
+      packed += v;
+      return;
+    }
+    if (v & 0x7FFu) atomicAdd(&s.cnt_w[sg], 1u);
+    if (v & (1u << 11)) atomicAdd(&s.cnt_bad[sg], 1u);
+    if (v & (1u << 22)) atomicAdd(&s.cnt_ins[sg], 1u);
+  }
+};
+
 template <bool XFER>
 __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinDesc& w, uint32_t i, uint32_t epoch,
-                                      bool ovf_mode, bool claim_free, bool any_hot) {
+                                      bool ovf_mode, bool claim_free, bool any_hot, SegTally& t) {
   const uint32_t b = s.batch[i];
   const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
   uint32_t cls = s.cls[i];
@@ -638,10 +667,13 @@ __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinD
     // singleton (:1255-1259, :1289-1290)
     if (is_w<XFER>(d, s, i, &cls, epoch, ovf_mode, claim_free, any_hot)) {
       s.cls[i] = cls | C_W | id_alone_bit<XFER>(s, i, cls, epoch, claim_free);
+      t.add(s, i, C_W, 0);
       return res_bad(s, i, cls, epoch);
     }
     const uint32_t code = s.code[i];
-    s.cls[i] = cls | (code == TB_CT_OK ? C_COMMIT : 0) | ((cls & C_INSERT) ? C_INSERTED : 0);
+    const uint32_t fin = cls | (code == TB_CT_OK ? C_COMMIT : 0) | ((cls & C_INSERT) ? C_INSERTED : 0);
+    s.cls[i] = fin;
+    t.add(s, i, fin, code);
     return false;
   }
   // chain head: members i..end, end = first unlinked event or the batch's last event (:1240-1300)
@@ -661,6 +693,7 @@ __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinD
     const uint32_t cj = s.cls[j];
     if (any_w) {
       s.cls[j] = cj | C_W | id_alone_bit<XFER>(s, j, cj, epoch, claim_free);
+      t.add(s, j, C_W, 0);
       continue;
     }
     uint32_t code = s.code[j];
@@ -672,22 +705,26 @@ __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinD
     s.code[j] = code;
     // members before the first failure ran ok before the rollback (their pulse_next ops stand)
     const uint32_t ranok = (f != NONE32 && j < f) ? C_RANOK : 0u;
-    s.cls[j] = cj | ranok | (commit ? C_COMMIT : 0) | ((commit && (cj & C_INSERT)) ? C_INSERTED : 0);
+    const uint32_t fin = cj | ranok | (commit ? C_COMMIT : 0) | ((commit && (cj & C_INSERT)) ? C_INSERTED : 0);
+    s.cls[j] = fin;
+    t.add(s, j, fin, code);
   }
   return any_w;  // a chain in W: walker
 }
 
 template <bool XFER>
 __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, uint32_t epoch) {
+  __shared__ uint32_t lds[4];
   if (WIN_REJECTED(d.g)) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  SegTally t{blockIdx.x * 256u / SEG, 0u};
   const bool ovf_mode = XFER && window_ovf_mode(d.g);
   bool bad = false;
   // transfer windows: claim-free (k_prep_reduce) skips the key-map reads, no hot account skips the
   // hot-mark reads
   const bool claim_free = XFER && (d.g->win_flags & 1u) != 0;
   const bool any_hot = !XFER || d.g->hot_count != 0;
-  if (i < w.E) bad = classify_event<XFER>(d, s, w, i, epoch, ovf_mode, claim_free, any_hot);
+  if (i < w.E) bad = classify_event<XFER>(d, s, w, i, epoch, ovf_mode, claim_free, any_hot, t);
   if (XFER && i == 0) {
     // the resolver's 128-bit signed arithmetic needs every balance sum below 2^126
     const u128 sum = d.g->ovf_bound + d.g->batch_amount_sum;
@@ -696,36 +733,20 @@ __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, u
   // a sticky flag: read before the atomic (same-address atomics from every wave serialize)
   if (XFER && __any(bad) && (threadIdx.x & 63) == 0 && !__hip_atomic_load(&d.g->res_inelig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
     atomicOr(&d.g->res_inelig, 1u);
+  // this block's share of its segment's counts (four blocks per segment)
+  const uint32_t c = block_sum<4>(t.packed, lds);
+  if (threadIdx.x == 0) {
+    if (c & 0x7FFu) atomicAdd(&s.cnt_w[t.seg], c & 0x7FFu);
+    if ((c >> 11) & 0x7FFu) atomicAdd(&s.cnt_bad[t.seg], (c >> 11) & 0x7FFu);
+    if (c >> 22) atomicAdd(&s.cnt_ins[t.seg], c >> 22);
+  }
 }
 
 #include "cpw.h"
 
 // ------------------------------------------------------------------------------------------------
-// Segment counts and the ordered W list (one event per thread, one 1024-event segment per block).
+// The ordered W list (one event per thread, one 1024-event segment per block; k_classify counted).
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(SEG) k_wcount(Scratch s, uint32_t E) {
-  __shared__ uint32_t lds[SEG / 64];
-  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
-  uint32_t nw = 0, nbad = 0, nins = 0;
-  if (i < E) {
-    const uint32_t cls = s.cls[i];
-    if (cls & C_W) {
-      nw = 1;
-    } else {
-      nbad = s.code[i] != TB_CT_OK;
-      nins = (cls & C_INSERTED) ? 1u : 0u;
-    }
-  }
-  nw = block_sum<SEG / 64>(nw, lds);
-  nbad = block_sum<SEG / 64>(nbad, lds);
-  nins = block_sum<SEG / 64>(nins, lds);
-  if (threadIdx.x == 0) {
-    s.cnt_w[blockIdx.x] = nw;
-    s.cnt_bad[blockIdx.x] = nbad;
-    s.cnt_ins[blockIdx.x] = nins;
-  }
-}
-
 __global__ void __launch_bounds__(SEG) k_wlist(Scratch s, uint32_t E) {
   __shared__ uint32_t lds[SEG / 64];
   if (s.cnt_w[blockIdx.x] == 0) return;  // uniform per block
