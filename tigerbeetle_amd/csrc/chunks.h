@@ -28,7 +28,7 @@
 #define RC_T 1024  // threads of the workgroup
 #define RC_ME (2 * RC_C)  // entries per chunk at most
 #define RC_LONG 8  // longer segments are walked by a whole wave
-// Entry encoding in LDS (k_rc_prep): bits 0-10 the (side, event) check slot (side << 10 | event in
+// Entry encoding in LDS (k_rc_build): bits 0-10 the (side, event) check slot (side << 10 | event in
 // chunk), bit 11 the entry's side checks (a limit), bit 12 a committed entry raises A.
 #define RC_EM_IDX 0x7FFu
 #define RC_EM_CHECK 0x800u
@@ -38,57 +38,19 @@
 #endif
 #define RC_NONE 0xFFFFu
 
-// Sorted (chunk, rank) pairs -> entries (meta, amount), chunk boundaries rc_cb[0..nch], and per
-// rank its account slot and initial A (written by the first entry of each (chunk, rank) segment:
-// identical values).
-__global__ void __launch_bounds__(256) k_rc_segs(Dev d, Scratch s, uint32_t n, uint32_t nch) {
-  const Globals* g = d.g;
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n || !g->res_chunked) return;
-  const uint32_t key = s.rkey[k];
-  const uint32_t cc = key == RC_DUMMY ? nch : key >> RC_RBITS;
-  uint32_t lo = 0;
-  if (k) {
-    const uint32_t kp = s.rkey[k - 1];
-    lo = (kp == RC_DUMMY ? nch : kp >> RC_RBITS) + 1u;
-  }
-  for (uint32_t c = lo; c <= cc; c++) s.rc_cb[c] = k;
-  if (k + 1 == n)
-    for (uint32_t c = cc + 1; c <= nch; c++) s.rc_cb[c] = n;
-  if (key == RC_DUMMY) return;
-  const uint32_t v = s.rval[k];
-  const uint32_t e = v >> 1, side = v & 1;
-  const uint32_t cls = s.cls[e];
-  const bool need_dr = cls & C_READS_DR, need_cr = cls & C_READS_CR;
-  const uint32_t slot = side ? s.cr_slot[e] : s.dr_slot[e];
-  const tb_account_t& a = d.acc[slot];
-  const bool dc = acc_is_dc(a.flags);
-  const bool pending = cls & C_PENDING;
-  const bool check = side ? need_cr : need_dr;
-  const bool add = !check && !pending && (side ? dc : !dc);
-  const bool wait = side ? need_dr : need_cr;
-  s.rmeta[k] = e | (side ? RM_SIDE : 0) | (check ? RM_CHECK : 0) | (wait ? RM_WAIT : 0) | (add ? RM_ADD : 0) |
-               (pending ? RM_PEND : 0);
-  s.ramt[k] = s.amt[e];
-  if (k == 0 || s.rkey[k - 1] != key) {
-    const __int128 dp = (__int128)U(a.debits_pending), dpo = (__int128)U(a.debits_posted);
-    const __int128 cp = (__int128)U(a.credits_pending), cpo = (__int128)U(a.credits_posted);
-    RState& rs = s.rstate[key & RC_RMASK];
-    rs.start = 0;
-    rs.end = 1;  // k_res_apply: the rank has entries
-    rs.slot = slot;
-    rs.A = dc ? cpo - dp - dpo : dpo - cp - cpo;
-    rs.d[0] = rs.d[1] = rs.d[2] = rs.d[3] = 0;
-  }
-}
-
-// Per chunk, precomputed by k_rc_prep (one workgroup per chunk, all chunks at once) so that the
-// single workgroup of k_rc_run only copies a chunk's tables into LDS (one barrier per chunk):
+// Per chunk, built by k_rc_build (one workgroup per chunk, all chunks at once) so that the single
+// workgroup of k_rc_run only copies a chunk's tables into LDS (one barrier per chunk). Chunk c owns
+// the entry range [cb, cb + 2 * RC_C), cb = 2 * c * RC_C (its events' two sides), of which the
+// first m = rc_cb[c] - cb are its hot entries, grouped by rank, event order inside a rank:
+//   rkey/rmeta/ramt[k] entry k: (chunk, rank) key (RC_DUMMY past the hot entries), meta, amount
 //   rc_segof[k]        entry k's segment within its chunk
 //   rc_seg[cb + c + i] segment i's first entry (i <= nseg; the last = the chunk's entry count)
 //   rc_list[cb + i]    segment ids: the > 64-entry segments, then the > RC_LONG ones, then the rest
 //   rc_ent[2e + side]  the entry of (event e, side) within its chunk (RC_NONE: that side is not hot)
+//   rc_em[k]           entry k's encoding (RC_EM_*)
 //   rc_cnt[c]          (nseg, huge, long, some amount >= 2^24)
+// and per rank (from the first entry of each (chunk, rank) segment: identical values) its account
+// slot and initial A in rstate.
 struct RcLds {
   int64_t A[RC_MAXR];          // available balance of every hot rank at the chunk start (clamped, below)
   uint64_t amt[RC_ME];         // the chunk's entries, grouped by rank, event order inside a rank
@@ -103,48 +65,112 @@ struct RcLds {
   uint16_t ent[2][RC_C];       // per side and event: its entry (RC_NONE: that side is not hot)
   uint8_t oth[RC_ME];          // per entry: the other side's check as its reader sees it (1 = pass)
   uint8_t cur[2 * RC_C], prv[2][RC_C];  // per (side, event): latest check / the one readers use (1 = pass)
-  uint32_t cb[1024 + 1];        // first entry of every chunk (no global load on a chunk's critical path)
+  uint32_t cb[1024];           // every chunk's end of hot entries (no global load on a chunk's critical path)
   uint32_t qlong, qshort, chg[2];
   uint32_t pmax;  // RC_PROF: longest wave walk of the iteration (cycles)
 };
 
-__global__ void __launch_bounds__(RC_T) k_rc_prep(Dev d, Scratch s, uint32_t E) {
-  __shared__ uint16_t rank[RC_ME];
+// The chunk's (side, event) pairs sorted by (rank, position) in LDS: a 2048-key bitonic sort of
+// rank << 11 | position (unique keys, so the order inside a rank is event order, as the stable global
+// sort it replaces gave), non-hot sides (rank 0xFFF) last. RC_MAXR = 4095 keeps 0xFFF free.
+__global__ void __launch_bounds__(RC_T) k_rc_build(Dev d, Scratch s, uint32_t E) {
+  __shared__ uint32_t sk[RC_ME];
   __shared__ uint16_t seg[RC_ME + 1];
   __shared__ uint32_t wcnt[2][RC_T / 64];
-  __shared__ uint32_t ncls[3], big;
+  __shared__ uint32_t ncls[3], big, mtot;
   if (!d.g->res_chunked) return;
   const uint32_t c = blockIdx.x, t = threadIdx.x;
   const int lane = t & 63;
   const uint32_t wave = t >> 6;
-  const uint32_t cb0 = s.rc_cb[c], m = s.rc_cb[c + 1] - cb0, c0 = c * RC_C;
-  if (c0 + t < E) *(uint32_t*)&s.rc_ent[2 * (c0 + t)] = (RC_NONE << 16) | RC_NONE;
+  const uint32_t c0 = c * RC_C, nev = min((uint32_t)RC_C, E - c0), n = 2 * nev, cb0 = 2 * c0;
+  if (t < nev) *(uint32_t*)&s.rc_ent[2 * (c0 + t)] = (RC_NONE << 16) | RC_NONE;
   if (t < 3) ncls[t] = 0;
-  if (t == 0) big = 0;
-  bool bg = false;
+  if (t == 0) {
+    big = 0;
+    mtot = 0;
+  }
 #pragma unroll
   for (int j = 0; j < 2; j++) {
-    const uint32_t kl = t + (uint32_t)j * RC_T;
-    if (kl < m) {
-      rank[kl] = (uint16_t)(s.rkey[cb0 + kl] & RC_RMASK);
-      bg = bg || (uint64_t)s.ramt[cb0 + kl] >= (1ull << 24);
+    const uint32_t p = t + (uint32_t)j * RC_T;
+    uint32_t v = 0xFFFFFFFFu;
+    if (p < n) {
+      const uint32_t key = s.rkey_in[cb0 + p];
+      v = ((key == RC_DUMMY ? 0xFFFu : (key & RC_RMASK)) << 11) | p;
     }
+    sk[p] = v;
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= RC_ME; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), l = i + j;
+      const uint32_t a = sk[i], b = sk[l];
+      if ((a > b) == ((i & k) == 0)) {
+        sk[i] = b;
+        sk[l] = a;
+      }
+      __syncthreads();
+    }
+  }
+  // the hot entries: m = the first non-hot position (sorted)
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const uint32_t q = t + (uint32_t)j * RC_T;
+    const bool hot = (sk[q] >> 11) < 0xFFFu;
+    const bool next_hot = q + 1 < RC_ME && (sk[q + 1] >> 11) < 0xFFFu;
+    if (hot && !next_hot) mtot = q + 1;
+  }
+  __syncthreads();
+  const uint32_t m = mtot;
+  bool bg = false, f[2];
+  uint32_t meta[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const uint32_t q = t + (uint32_t)j * RC_T;
+    f[j] = false;
+    meta[j] = 0;
+    if (q >= n) continue;
+    const uint32_t k = cb0 + q;
+    if (q >= m) {
+      s.rkey[k] = RC_DUMMY;
+      continue;
+    }
+    const uint32_t r = sk[q] >> 11, pos = sk[q] & 0x7FFu;
+    const uint32_t e = c0 + (pos >> 1), side = pos & 1u;
+    const uint32_t key = (c << RC_RBITS) | r;
+    s.rkey[k] = key;
+    // entry meta and amount (the relaxation's k_res_segs, chunk layout)
+    const uint32_t cls = s.cls[e];
+    const bool need_dr = cls & C_READS_DR, need_cr = cls & C_READS_CR;
+    const uint32_t slot = side ? s.cr_slot[e] : s.dr_slot[e];
+    const tb_account_t& a = d.acc[slot];
+    const bool dc = acc_is_dc(a.flags);
+    const bool pending = cls & C_PENDING;
+    const bool check = side ? need_cr : need_dr;
+    const bool add = !check && !pending && (side ? dc : !dc);
+    const bool wait = side ? need_dr : need_cr;
+    meta[j] = e | (side ? RM_SIDE : 0) | (check ? RM_CHECK : 0) | (wait ? RM_WAIT : 0) | (add ? RM_ADD : 0) |
+              (pending ? RM_PEND : 0);
+    s.rmeta[k] = meta[j];
+    const u128 amt = s.amt[e];
+    s.ramt[k] = amt;
+    bg = bg || (uint64_t)amt >= (1ull << 24);
+    f[j] = q == 0 || (sk[q - 1] >> 11) != r;
+    if (f[j]) {
+      const __int128 dp = (__int128)U(a.debits_pending), dpo = (__int128)U(a.debits_posted);
+      const __int128 cp = (__int128)U(a.credits_pending), cpo = (__int128)U(a.credits_posted);
+      RState& rs = s.rstate[r];
+      rs.start = 0;
+      rs.end = 1;  // k_res_apply: the rank has entries
+      rs.slot = slot;
+      rs.A = dc ? cpo - dp - dpo : dpo - cp - cpo;
+      rs.d[0] = rs.d[1] = rs.d[2] = rs.d[3] = 0;
+    }
+    s.rc_ent[2 * e + side] = (uint16_t)q;
+    s.rc_em[k] = (uint16_t)((side << 10) | (e - c0) | ((meta[j] & RM_CHECK) ? RC_EM_CHECK : 0u) |
+                            ((meta[j] & RM_ADD) ? RC_EM_ADD : 0u));
   }
   if (bg) big = 1;
-  __syncthreads();
-  bool f[2];
-#pragma unroll
-  for (int j = 0; j < 2; j++) {
-    const uint32_t kl = t + (uint32_t)j * RC_T;
-    f[j] = kl < m && (kl == 0 || rank[kl] != rank[kl - 1]);
-    if (kl < m) {
-      const uint32_t meta = s.rmeta[cb0 + kl];
-      const uint32_t side = (meta & RM_SIDE) ? 1u : 0u;
-      s.rc_ent[2 * (meta & RM_EVENT) + side] = (uint16_t)kl;
-      s.rc_em[cb0 + kl] = (uint16_t)((side << 10) | ((meta & RM_EVENT) - c0) | ((meta & RM_CHECK) ? RC_EM_CHECK : 0u) |
-                                     ((meta & RM_ADD) ? RC_EM_ADD : 0u));
-    }
-  }
+  // segments: their starts, each entry's segment, and the walk lists (huge, long, short)
   const unsigned long long b0 = __ballot(f[0]), b1 = __ballot(f[1]);
   if (lane == 0) {
     wcnt[0][wave] = (uint32_t)__popcll(b0);
@@ -169,16 +195,16 @@ __global__ void __launch_bounds__(RC_T) k_rc_prep(Dev d, Scratch s, uint32_t E) 
   const uint32_t nseg = tot0 + tot1;
   if (t == 0) seg[nseg] = (uint16_t)m;
   __syncthreads();
-  uint32_t cls[2], idx[2];
+  uint32_t cl[2], idx[2];
 #pragma unroll
   for (int j = 0; j < 2; j++) {
     const uint32_t sg = t + (uint32_t)j * RC_T;
-    cls[j] = 3;
+    cl[j] = 3;
     if (sg <= nseg) s.rc_seg[cb0 + c + sg] = seg[sg];
     if (sg < nseg) {
       const uint32_t len = (uint32_t)(seg[sg + 1] - seg[sg]);
-      cls[j] = len > 64 ? 0u : (len > RC_LONG ? 1u : 2u);
-      idx[j] = atomicAdd(&ncls[cls[j]], 1u);
+      cl[j] = len > 64 ? 0u : (len > RC_LONG ? 1u : 2u);
+      idx[j] = atomicAdd(&ncls[cl[j]], 1u);
     }
   }
   __syncthreads();
@@ -186,9 +212,12 @@ __global__ void __launch_bounds__(RC_T) k_rc_prep(Dev d, Scratch s, uint32_t E) 
 #pragma unroll
   for (int j = 0; j < 2; j++) {
     const uint32_t sg = t + (uint32_t)j * RC_T;
-    if (cls[j] < 3) s.rc_list[cb0 + (cls[j] == 0 ? 0u : (cls[j] == 1 ? nh : nh + nl)) + idx[j]] = (uint16_t)sg;
+    if (cl[j] < 3) s.rc_list[cb0 + (cl[j] == 0 ? 0u : (cl[j] == 1 ? nh : nh + nl)) + idx[j]] = (uint16_t)sg;
   }
-  if (t == 0) s.rc_cnt[c] = make_uint4(nseg, nh, nl, big);
+  if (t == 0) {
+    s.rc_cnt[c] = make_uint4(nseg, nh, nl, big);
+    s.rc_cb[c] = cb0 + m;  // the end of the chunk's hot entries
+  }
 }
 
 // A is the pre-window balance clamped into [-2^62, 2^62] plus the window's effects so far: a check
@@ -391,7 +420,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   uint64_t prof[4] = {0, 0, 0, 0};
   uint64_t wrounds = 0, wt[2] = {0, 0}, hz[4] = {0, 0, 0, 0};  // RC_PROF: huge walks (cycles, steps) it 0 / later
   for (uint32_t r = t; r < R; r += RC_T) L.A[r] = rc_clamp(s.rstate[r].A);
-  for (uint32_t c = t; c <= nch; c += RC_T) L.cb[c] = s.rc_cb[c];
+  for (uint32_t c = t; c < nch; c += RC_T) L.cb[c] = s.rc_cb[c];  // chunk ends (k_rc_build)
   __syncthreads();
   // the next chunk's entries and tables, loaded one chunk ahead (two of each per thread)
   uint32_t pk[2] = {0, 0}, pe = 0;
@@ -400,7 +429,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   uint16_t ps[2] = {0, 0}, pg[2] = {0, 0}, pl[2] = {0, 0};
   uint4 pc = make_uint4(0, 0, 0, 0);
   auto fetch = [&](uint32_t c) {
-    const uint32_t b0 = L.cb[c], b1 = L.cb[c + 1];
+    const uint32_t b0 = 2 * c * RC_C, b1 = L.cb[c];
     pc = s.rc_cnt[c];
 #pragma unroll
     for (int j = 0; j < 2; j++) {
@@ -419,7 +448,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   fetch(0);
   uint64_t iters = 0;
   for (uint32_t c = 0; c < nch; c++) {
-    const uint32_t cb0 = L.cb[c], m = L.cb[c + 1] - cb0;
+    const uint32_t cb0 = 2 * c * RC_C, m = L.cb[c] - cb0;
     const uint32_t c0 = c * RC_C;
     const uint32_t nseg = rc_uniform(pc.x), nhuge = rc_uniform(pc.y), nlong = nhuge + rc_uniform(pc.z);
     const bool big = rc_uniform(pc.w) != 0;

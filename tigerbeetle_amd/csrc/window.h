@@ -109,8 +109,8 @@ struct Scratch {
   // (debits of a debits<=credits account, credits of a credits<=debits one; bit 63 = must stay hot)
   uint32_t* bind_slot;
   unsigned long long* bind_adv;
-  // chunked resolver (chunks.h): first sorted entry of each 1024-event chunk, and the per-chunk
-  // tables k_rc_prep builds (segment of each entry, segment starts, walk lists, entry of each event
+  // chunked resolver (chunks.h): the end of each 1024-event chunk's hot entries, and the per-chunk
+  // tables k_rc_build builds (segment of each entry, segment starts, walk lists, entry of each event
   // side, counts)
   uint32_t* rc_cb;
   uint16_t *rc_segof, *rc_seg, *rc_list, *rc_ent, *rc_em;
