@@ -100,10 +100,19 @@ __device__ inline uint32_t acc_probe_from(const AccEntry* __restrict__ tab, uint
 // A balance-reading decision makes the read account hot for this window: every event touching it
 // is then decided in order (resolver.h or the walker). The first marker assigns the account its
 // dense rank (one counter atomic per wave).
-__device__ inline void mark_hot(Dev d, Scratch s, uint32_t slot, uint32_t epoch) {
+// blk: this block's claimed slots (LDS, MARK_LDS entries): at most one lane per block and account
+// goes on to the global exchange (Zipf-hot accounts would serialize every marking lane on one word).
+#define MARK_LDS 512
+__device__ inline void mark_hot(Dev d, Scratch s, uint32_t slot, uint32_t epoch, uint32_t* blk) {
   // a plain read first: a hot account is marked by many events (a stale read only costs the atomic)
-  bool first = false;
-  if (d.hot[slot] != epoch) first = atomicExch(&d.hot[slot], epoch) != epoch;
+  if (d.hot[slot] == epoch) return;
+  uint32_t h = (slot * 2654435761u) & (MARK_LDS - 1);
+  for (int probe = 0; probe < 8; probe++, h = (h + 1) & (MARK_LDS - 1)) {
+    const uint32_t k = atomicCAS(&blk[h], NONE32, slot);
+    if (k == NONE32) break;  // this lane marks it for the block
+    if (k == slot) return;   // another lane of the block does
+  }
+  const bool first = atomicExch(&d.hot[slot], epoch) != epoch;
   const unsigned long long m = __ballot(first);
   if (!first) return;
   const int lane = threadIdx.x & 63;
@@ -129,7 +138,8 @@ __device__ inline void mark_hot(Dev d, Scratch s, uint32_t slot, uint32_t epoch)
 // add per distinct rank per block: Zipf-hot accounts would serialize on one address otherwise),
 // k_bind_decide un-marks the non-binding accounts, k_classify then drops their read bits.
 // ------------------------------------------------------------------------------------------------
-#define BIND_LDS 1024
+#define BIND_LDS 4096
+#define BIND_T 1024  // threads (events) per k_bind_sum block
 #define BIND_FORCE (1ull << 63)
 #define BIND_AMOUNT_MAX (1ull << 40)  // larger amounts keep their account hot (the sums stay < 2^63)
 
@@ -153,7 +163,7 @@ __device__ inline void bind_add(Dev d, Scratch s, uint32_t* tk, unsigned long lo
   atomicAdd(&s.bind_adv[r], v);  // LDS table crowded: straight to memory
 }
 
-__global__ void __launch_bounds__(256) k_bind_sum(Dev d, Scratch s, uint32_t E, uint32_t epoch) {
+__global__ void __launch_bounds__(BIND_T) k_bind_sum(Dev d, Scratch s, uint32_t E, uint32_t epoch) {
   __shared__ uint32_t tk[BIND_LDS];
   __shared__ unsigned long long tv[BIND_LDS];
   if (WIN_REJECTED(d.g) || !d.g->hot_count) return;
@@ -228,8 +238,10 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   // bit 0 huge amount, bit 1 not claim-free, bit 2 first id above every stored id, bit 3 pulse_next op
   __shared__ uint32_t aux;
   __shared__ unsigned long long id_max;  // largest id key this block may insert (Globals::x_id_max)
+  __shared__ uint32_t marked[MARK_LDS];  // mark_hot: accounts this block marks
   if (WIN_REJECTED(d.g)) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t j = threadIdx.x; j < MARK_LDS; j += blockDim.x) marked[j] = NONE32;
   if (threadIdx.x == 0) {
     aux = 0;
     id_max = 0;
@@ -408,8 +420,8 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     }
     prec = (cls & C_PREP_REC) != 0;
     // Hot marks: the first marker of an account this window gives it the next dense rank.
-    if (cls & C_READS_DR) mark_hot(d, s, dr_slot, epoch);
-    if (cls & C_READS_CR) mark_hot(d, s, cr_slot, epoch);
+    if (cls & C_READS_DR) mark_hot(d, s, dr_slot, epoch, marked);
+    if (cls & C_READS_CR) mark_hot(d, s, cr_slot, epoch, marked);
     s.code[i] = code;
     s.cls[i] = cls;
     s.batch[i] = (uint16_t)b;
