@@ -128,7 +128,11 @@ __device__ __attribute__((always_inline)) inline tb_transfer_t pv_record(const t
   t2.id = t.id;
   t2.debit_account_id = p.debit_account_id;
   t2.credit_account_id = p.credit_account_id;
-  t2.user_data_128 = U(t.user_data_128) > 0 ? t.user_data_128 : p.user_data_128;
+  // (selects on the 64-bit words: a select between the two struct members would be one between
+  // their addresses, which keeps both records in scratch memory instead of registers)
+  const bool own128 = (t.user_data_128.lo | t.user_data_128.hi) != 0;
+  t2.user_data_128.lo = own128 ? t.user_data_128.lo : p.user_data_128.lo;
+  t2.user_data_128.hi = own128 ? t.user_data_128.hi : p.user_data_128.hi;
   t2.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
   t2.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
   t2.ledger = p.ledger;
