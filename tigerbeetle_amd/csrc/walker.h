@@ -80,6 +80,8 @@ __device__ inline void bmap_set_committed(BEntry* bm, uint32_t e, uint32_t epoch
 struct WPre {
   uint32_t i, cls, b, code, id_tslot, id_ent, dr, cr, p_tslot, pid_ent;
   bool id_alone;  // no other event of the window carries this id: no earlier commit of it to look up
+  uint4 head;     // transfers: the event's first 16 B (its id), loaded one event ahead: the load brings
+                  // the record's line into the cache, so the rest of it is a cache hit when it runs
 };
 
 struct Walker {
@@ -219,6 +221,7 @@ struct Walker {
       e.cr = s.cr_slot[i];
       e.p_tslot = s.p_tslot[i];
       e.pid_ent = s.pid_ent[i];
+      e.head = reinterpret_cast<const uint4*>(ev)[(size_t)i * 8];
     }
     e.id_alone = (e.cls & C_IDALONE) != 0;  // k_classify
     return e;
@@ -229,6 +232,8 @@ struct Walker {
     const uint32_t i = e.i;
     if (e.cls & C_STATIC) return e.code;
     tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev)[i];
+    t.id.lo = ((uint64_t)e.head.y << 32) | e.head.x;
+    t.id.hi = ((uint64_t)e.head.w << 32) | e.head.z;
     t.timestamp = win_ts(*w, e.b, i);
     if (e.cls & C_POSTVOID) return post_or_void(e, t);
     if (e.id_tslot != NONE32) return ct_exists(t, d.xr[e.id_tslot]);
