@@ -1155,11 +1155,35 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     ins = (cls & C_W) ? s.ins[i] != 0 : (cls & C_INSERTED) != 0;
   }
   const uint32_t bad = code != TB_CT_OK;
-  const uint32_t pbad = seg_prefix<SEG>(s.cnt_bad, blockIdx.x, lds);
-  const uint32_t pins = seg_prefix<SEG>(s.cnt_ins, blockIdx.x, lds);
-  uint32_t tot_bad, tot_ins;
-  const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
-  const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
+  // The earlier segments' failure and insert counts, and this event's ranks inside the segment, in
+  // one pass with one barrier: per wave the segment-count partials (each < 2^21, packed in 64 bits)
+  // and the in-segment scan of bad << 16 | inserted (each <= SEG).
+  uint32_t rbad, rins;
+  {
+    const uint32_t wave = threadIdx.x >> 6;
+    uint32_t vb = 0, vi = 0;
+    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += SEG) {
+      vb += s.cnt_bad[j];
+      vi += s.cnt_ins[j];
+    }
+    const unsigned long long segp = ((unsigned long long)wave_sum(vb) << 32) | wave_sum(vi);
+    const uint32_t mine = (bad << 16) | (ins ? 1u : 0u);
+    const uint32_t inc = wave_incl_scan(mine);
+    if (lane == 63) lds[wave] = inc;
+    if (lane == 0) ldsm[wave] = segp;
+    __syncthreads();
+    uint32_t wp = 0;
+    unsigned long long sp = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SEG / 64; k++) {
+      if (k < wave) wp += lds[k];
+      sp += ldsm[k];
+    }
+    __syncthreads();  // lds / ldsm are reused below
+    const uint32_t ex = wp + inc - mine;
+    rbad = (uint32_t)(sp >> 32) + (ex >> 16);
+    rins = (uint32_t)sp + (ex & 0xFFFFu);
+  }
   const uint64_t xbase = d.g->base;
   // k_ct_prep already stored the stamped input record of each plain create it expected to insert
   // at its own position (base + i). That record is final when the event inserts at rank i (no

@@ -147,20 +147,21 @@ __device__ __forceinline__ void wave_sync() {
 // ------------------------------------------------------------------------------------------------
 // Scan helpers (wave64 shuffles + one LDS word per wave).
 // ------------------------------------------------------------------------------------------------
+// Inclusive wave64 scan with DPP row shifts and row broadcasts (six VALU adds, no LDS round trip:
+// a __shfl is a ds_bpermute through the LDS unit).
 __device__ inline uint32_t wave_incl_scan(uint32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(v, o, 64);
-    if (lane >= o) v += y;
-  }
-  return v;
+  int32_t x = (int32_t)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)x;
 }
 
 __device__ inline uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
 }
 
 // Exclusive prefix over the threads of a block of `nwaves` waves; *total = block sum.
