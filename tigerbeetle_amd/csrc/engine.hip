@@ -119,7 +119,7 @@ __device__ inline void mark_hot(Dev d, Scratch s, uint32_t slot, uint32_t epoch,
   const int leader = __builtin_ctzll(m);
   uint32_t base = 0;
   if (lane == leader) base = atomicAdd(&d.g->hot_count, (uint32_t)__popcll(m));
-  base = __shfl(base, leader, 64);
+  base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);  // (leader is wave-uniform)
   const uint32_t rank = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
   d.hot_rank[slot] = rank;
   s.bind_slot[rank] = slot;
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(256) k_bind_decide(Dev d, Scratch s) {
     const int leader = __builtin_ctzll(live);
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(&g->hot_live, (uint32_t)__popcll(live));
-    base = __shfl(base, leader, 64);
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);  // (leader is wave-uniform)
     if (r < n && !cold) d.hot_rank[s.bind_slot[r]] = base + (uint32_t)__popcll(live & ((1ull << lane) - 1));
   }
 }
@@ -1327,13 +1327,14 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
       unsigned long long q = 0;
       if ((int)lane == leader)
         q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), (unsigned long long)__popcll(m));
-      q = __shfl(q, leader, 64);
+      q = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(q >> 32), leader) << 32) |
+          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q, leader);
       if (xapp) d.exp[*d.exp_cur][q + (unsigned long long)__popcll(m & ((1ull << lane) - 1))] = xent;
     }
   }
   // Compact this wave's inserted records in LDS, then store them as one contiguous run (a wave
   // with only in-place records stores nothing).
-  const uint32_t r0 = __shfl(rins, 0);
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, 0);
   const uint32_t nins = wave_rec ? (uint32_t)__popcll(__ballot(ins)) : 0u;
   wave_sync();
   if (ins && wave_rec) {

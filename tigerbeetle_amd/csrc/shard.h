@@ -613,7 +613,7 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
     const unsigned long long m = block_max_u64<SEG / 64>(key, ldsm);
     if (threadIdx.x == 0 && m > g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&g->x_id_max), m);
   }
-  const uint32_t r0 = __shfl(rins, 0);  // the wave's first insert rank (all lanes active here)
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, 0);  // the wave's first insert rank (all lanes active here)
   if (commit) {
     if (XFER) {
       uint32_t drs = (roles & ROLE_DR) ? s.dr_slot[i] : NONE32, crs = (roles & ROLE_CR) ? s.cr_slot[i] : NONE32;
