@@ -901,19 +901,33 @@ __device__ inline unsigned long long block_min_u64(unsigned long long v, unsigne
   return ~block_max_u64<NWAVES>(~v, lds);
 }
 
+// A u64 through one DPP move per 32-bit half; lanes without a source lane get ~0 (the min identity).
+template <int CTRL, int ROWS>
+__device__ inline unsigned long long dpp_mov_u64(unsigned long long x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)x, CTRL, ROWS, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)(x >> 32), CTRL, ROWS, 0xf, false);
+  return ((unsigned long long)hi << 32) | lo;
+}
+template <int CTRL, int ROWS>
+__device__ inline unsigned long long dpp_min_u64(unsigned long long x) {
+  return umin64(x, dpp_mov_u64<CTRL, ROWS>(x));
+}
+
 // Exclusive prefix minimum over the block's threads (identity ~0); *total = the block minimum.
 template <int NWAVES>
 __device__ inline unsigned long long block_excl_min_u64(unsigned long long v, unsigned long long* lds,
                                                         unsigned long long* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // inclusive wave scan with DPP (row shifts, row broadcasts; lanes without a source keep the
+  // identity), then the exclusive value by a wave shift right by one
   unsigned long long inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc = umin64(inc, y);
-  }
-  unsigned long long ex = __shfl_up(inc, 1, 64);
-  if (lane == 0) ex = ~0ull;
+  inc = dpp_min_u64<0x111, 0xf>(inc);  // row_shr:1
+  inc = dpp_min_u64<0x112, 0xf>(inc);  // row_shr:2
+  inc = dpp_min_u64<0x114, 0xf>(inc);  // row_shr:4
+  inc = dpp_min_u64<0x118, 0xf>(inc);  // row_shr:8
+  inc = dpp_min_u64<0x142, 0xa>(inc);  // row_bcast:15
+  inc = dpp_min_u64<0x143, 0xc>(inc);  // row_bcast:31
+  const unsigned long long ex = dpp_mov_u64<0x138, 0xf>(inc);  // wave_shr:1 (lane 0: ~0)
   if (lane == 63) lds[wave] = inc;
   __syncthreads();
   unsigned long long wp = ~0ull, tot = ~0ull;
