@@ -98,29 +98,23 @@ __device__ inline uint32_t acc_probe_from(const AccEntry* __restrict__ tab, uint
 }
 
 // A balance-reading decision makes the read account hot for this window: every event touching it
-// is then decided in order (resolver.h or the walker). The first marker assigns the account its
-// dense rank (one counter atomic per wave).
+// is then decided in order (resolver.h or the walker). The first marker gets the account a dense
+// rank (k_ct_prep: one counter atomic per block, after its marks).
 // blk: this block's claimed slots (LDS, MARK_LDS entries): at most one lane per block and account
 // goes on to the global exchange (Zipf-hot accounts would serialize every marking lane on one word).
 #define MARK_LDS 512
-__device__ inline void mark_hot(Dev d, Scratch s, uint32_t slot, uint32_t epoch, uint32_t* blk) {
+__device__ inline bool mark_first(Dev d, uint32_t slot, uint32_t epoch, uint32_t* blk) {
   // a plain read first: a hot account is marked by many events (a stale read only costs the atomic)
-  if (d.hot[slot] == epoch) return;
+  if (d.hot[slot] == epoch) return false;
   uint32_t h = (slot * 2654435761u) & (MARK_LDS - 1);
   for (int probe = 0; probe < 8; probe++, h = (h + 1) & (MARK_LDS - 1)) {
     const uint32_t k = atomicCAS(&blk[h], NONE32, slot);
     if (k == NONE32) break;  // this lane marks it for the block
-    if (k == slot) return;   // another lane of the block does
+    if (k == slot) return false;   // another lane of the block does
   }
-  const bool first = atomicExch(&d.hot[slot], epoch) != epoch;
-  const unsigned long long m = __ballot(first);
-  if (!first) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __builtin_ctzll(m);
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(&d.g->hot_count, (uint32_t)__popcll(m));
-  base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);  // (leader is wave-uniform)
-  const uint32_t rank = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+  return atomicExch(&d.hot[slot], epoch) != epoch;
+}
+__device__ inline void hot_rank_set(Dev d, Scratch s, uint32_t slot, uint32_t rank) {
   d.hot_rank[slot] = rank;
   s.bind_slot[rank] = slot;
   s.bind_adv[rank] = 0;
@@ -238,15 +232,18 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   // bit 0 huge amount, bit 1 not claim-free, bit 2 first id above every stored id, bit 3 pulse_next op
   __shared__ uint32_t aux;
   __shared__ unsigned long long id_max;  // largest id key this block may insert (Globals::x_id_max)
-  __shared__ uint32_t marked[MARK_LDS];  // mark_hot: accounts this block marks
+  __shared__ uint32_t marked[MARK_LDS];  // mark_first: accounts this block marks
+  __shared__ uint32_t nfirst, fbase;      // accounts this block marked first, their first rank
   if (WIN_REJECTED(d.g)) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   for (uint32_t j = threadIdx.x; j < MARK_LDS; j += blockDim.x) marked[j] = NONE32;
   if (threadIdx.x == 0) {
     aux = 0;
     id_max = 0;
+    nfirst = 0;
   }
   __syncthreads();
+  uint32_t first_slot[2] = {NONE32, NONE32};  // accounts this event marked first (debit, credit side)
   u128 amount_upper = 0;
   tb_transfer_t t;  // the event, stamped (also the record a plain create stores in place)
   bool prec = false;
@@ -420,8 +417,8 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     }
     prec = (cls & C_PREP_REC) != 0;
     // Hot marks: the first marker of an account this window gives it the next dense rank.
-    if (cls & C_READS_DR) mark_hot(d, s, dr_slot, epoch, marked);
-    if (cls & C_READS_CR) mark_hot(d, s, cr_slot, epoch, marked);
+    if ((cls & C_READS_DR) && mark_first(d, dr_slot, epoch, marked)) first_slot[0] = dr_slot;
+    if ((cls & C_READS_CR) && mark_first(d, cr_slot, epoch, marked)) first_slot[1] = cr_slot;
     s.code[i] = code;
     s.cls[i] = cls;
     s.batch[i] = (uint16_t)b;
@@ -460,6 +457,19 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   }
   // Window amount bound: block reduction into this block's partial (k_prep_reduce sums them; a
   // same-address atomic per block serializes thousands of blocks on one memory-side word).
+  {
+    // dense ranks for the accounts this block marked first: one counter atomic per block
+    const bool f0 = first_slot[0] != NONE32, f1 = first_slot[1] != NONE32;
+    uint32_t k0 = 0, k1 = 0;
+    if (f0) k0 = atomicAdd(&nfirst, 1u);
+    if (f1) k1 = atomicAdd(&nfirst, 1u);
+    if (__syncthreads_or(f0 || f1)) {
+      if (threadIdx.x == 0) fbase = atomicAdd(&d.g->hot_count, nfirst);
+      __syncthreads();
+      if (f0) hot_rank_set(d, s, first_slot[0], fbase + k0);
+      if (f1) hot_rank_set(d, s, first_slot[1], fbase + k1);
+    }
+  }
   red[threadIdx.x] = ((uint64_t)(amount_upper >> 64) != 0) ? 0 : amount_upper;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
