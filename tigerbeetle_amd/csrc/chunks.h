@@ -599,3 +599,38 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
     g->res_chunk_windows++;
   }
 }
+
+// Chunked windows: each account's committed effects per field, summed per 1024-entry block in LDS
+// (the entries are sorted by (chunk, rank): a block holds runs of equal keys; one LDS add per entry,
+// then one global add per run and field). Per-wave segment atomics would put every wave of the
+// Zipf head's runs on the same four words. Sums stay below 2^62 (rc_eligible), so 64-bit adds.
+__global__ void __launch_bounds__(1024) k_rc_sum(Dev d, Scratch s, uint32_t n) {
+  __shared__ unsigned long long sums[1024][4];
+  __shared__ uint32_t runkey[1024];
+  __shared__ uint32_t lds[1024 / 64];
+  const Globals* g = d.g;
+  if (g->res_inelig || !g->hot_count || g->res_error || !g->res_chunked) return;
+  const uint32_t k = blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t key = k < n ? s.rkey[k] : RC_DUMMY;
+  const bool live = key != RC_DUMMY;
+  const bool start = live && (threadIdx.x == 0 || s.rkey[k - 1] != key);
+  uint32_t nrun;
+  const uint32_t excl = block_excl<1024 / 64>(start ? 1u : 0u, lds, &nrun);
+  const uint32_t run = excl + (start ? 1u : 0u) - 1u;  // live entries: the run they belong to
+  if (start) runkey[run] = key;
+  if (threadIdx.x < nrun) sums[threadIdx.x][0] = sums[threadIdx.x][1] = sums[threadIdx.x][2] = sums[threadIdx.x][3] = 0;
+  __syncthreads();
+  if (live && s.rown[k] != 0u) {
+    const uint32_t meta = s.rmeta[k];
+    atomicAdd(&sums[run][rm_field(meta)], (unsigned long long)(uint64_t)s.ramt[k]);
+  }
+  __syncthreads();
+  if (threadIdx.x < nrun) {
+    RState& rs = s.rstate[runkey[threadIdx.x] & RC_RMASK];
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+      const unsigned long long v = sums[threadIdx.x][f];
+      if (v) atomic_add_u128((tb_uint128_t*)&rs.d[f], (u128)v);
+    }
+  }
+}
