@@ -26,8 +26,9 @@ def _submit(gpu, op, batches, tick_ns):
     data = np.concatenate([np.frombuffer(ev.tobytes(), np.uint8) for ev in batches])
     h_ev = torch.empty(max(len(data), 128), dtype=torch.uint8, pin_memory=True)
     h_ev[: len(data)] = torch.from_numpy(data.copy())
-    h_res = torch.zeros(max(sum(ns), 1) * 8, dtype=torch.uint8, pin_memory=True)
-    h_base = torch.zeros(len(ns) + 1, dtype=torch.int32, pin_memory=True)
+    # 0xFF until the window's D2H lands (a reply read too early cannot look right)
+    h_res = torch.full((max(sum(ns), 1) * 8,), 0xFF, dtype=torch.uint8, pin_memory=True)
+    h_base = torch.full((len(ns) + 1,), -1, dtype=torch.int32, pin_memory=True)
     t = gpu.commit_window_host(op, h_ev.data_ptr(), ns, ts, h_res.data_ptr(), h_base.data_ptr(), True, ts[0])
     return t, (h_ev, h_res, h_base), len(ns)
 
@@ -94,6 +95,48 @@ def test_host_fed_uniform_128_batch_windows():
         gpu.sync()
         for (t, bufs, nb), batches in subs:
             assert _replies(bufs, nb) == oracle_batches(ref, Operation.create_transfers, batches)
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_host_fed_done_is_per_ticket():
+    """tbg_host_window_done(t) may report 1 only once window t's replies have landed, also after two
+    later windows were submitted on its slot: a large window (a ~128 MB H2D) followed at
+    once by two tiny ones; whenever done(t) says 1, the reply buffers (pre-filled with 0xFF) must hold
+    the final bytes, and done is monotone in the ticket order."""
+    from tigerbeetle_amd import StateMachine
+
+    bm, n_acc, win = 8190, 100_000, 128
+    gpu = StateMachine(batch_max=bm, accounts_max=n_acc, transfers_max=2 * win * bm, window_events_max=win * bm)
+    ref = OracleStateMachine(batch_max=bm)
+    try:
+        acc = workload.accounts(0, n_acc, seed=62)
+        ab = [acc[i:i + bm] for i in range(0, n_acc, bm)]
+        t, bufs, nb = _submit(gpu, Operation.create_accounts, ab, 0)
+        gpu.sync()
+        assert _replies(bufs, nb) == oracle_batches(ref, Operation.create_accounts, ab)
+        xf = workload.transfers_uniform(0, win * bm + 2, 62, n_acc)
+        big = [xf[b * bm:(b + 1) * bm] for b in range(win)]
+        small = [[xf[win * bm:win * bm + 1]], [xf[win * bm + 1:win * bm + 2]]]
+        subs = [_submit(gpu, Operation.create_transfers, big, 0)]
+        for s in small:
+            subs.append(_submit(gpu, Operation.create_transfers, s, 0))
+        expect = [oracle_batches(ref, Operation.create_transfers, w) for w in [big] + small]
+        for _ in range(200000):
+            done = [gpu.window_done(s[0]) for s in subs]
+            for k in range(3):
+                if done[k]:
+                    assert _replies(subs[k][1], subs[k][2]) == expect[k], f"ticket {k}: done before its replies"
+            assert all(done[k] or not done[k + 1] for k in range(2)), done
+            if all(done):
+                break
+        gpu.sync()
+        assert all(gpu.window_done(s[0]) for s in subs)
+        for k in range(3):
+            assert _replies(subs[k][1], subs[k][2]) == expect[k]
         _compare_final(gpu, ref)
     finally:
         gpu.close()

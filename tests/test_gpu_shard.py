@@ -26,6 +26,7 @@ class LocalShards:
                                            transfers_max=transfers_max, window_events_max=window_events_max)
                        for r in range(G)]
         self.prepare_timestamp = 0
+        self.pulse_log = []  # (T, pulse()) before every batch, the harness order (:2719-2739)
 
     def close(self):
         for s in self.shards:
@@ -44,10 +45,22 @@ class LocalShards:
             t.copy_(total)
         torch.cuda.synchronize()
 
+    def pulse_before(self, T):
+        """The harness pulse before a batch at T (state_machine.zig:2719-2739): pulse() on the
+        shards, and when it is true commit(.pulse) at T through the general path."""
+        from tigerbeetle_amd.sharding import pulse_general
+
+        due = self.shards[0].pulse(T)
+        assert all(s.pulse(T) == due for s in self.shards)
+        if due:
+            pulse_general(self.shards, self.summed, T)
+        return due
+
     def commit_any(self, op, batches, tick_ns=0):
-        """A window through the order-free path when no pulse can be due in it, else (or when the
-        window is outside the order-free class) batch by batch through the general path
-        (csrc/shard_gx.inc). Returns (per-batch replies, took the fast path)."""
+        """A window through the order-free path when no pulse can be due in it (after the harness
+        pulse before its first batch), else (or when the window is outside the order-free class)
+        batch by batch through the general path (csrc/shard_gx.inc). Returns (per-batch replies,
+        took the fast path)."""
         import torch
 
         from tigerbeetle_amd._lib import UnsupportedWindow
@@ -55,9 +68,13 @@ class LocalShards:
 
         ts0 = self.prepare_timestamp
         t_last = ts0 + tick_ns + sum(1 + len(ev) for ev in batches)
+        log0 = len(self.pulse_log)
+        if batches:
+            T0 = ts0 + tick_ns + 1 + len(batches[0])
+            self.pulse_log.append((T0, self.pulse_before(T0)))
         if t_last < self.shards[0].pulse_next():
             try:
-                return self.commit_window(op, batches, tick_ns), True
+                return self.commit_window(op, batches, tick_ns, _pulsed=True), True
             except UnsupportedWindow:
                 for s in self.shards:  # every shard reports the rejected window once
                     try:
@@ -65,20 +82,24 @@ class LocalShards:
                     except UnsupportedWindow:
                         pass
                 self.prepare_timestamp = ts0
+        del self.pulse_log[log0 + 1:]
         out = []
         self.prepare_timestamp = ts0 + tick_ns
-        for ev in batches:
+        for k, ev in enumerate(batches):
             self.prepare_timestamp += 1 + len(ev)
+            if k > 0:  # batch 0's pulse ran above
+                self.pulse_log.append((self.prepare_timestamp, self.pulse_before(self.prepare_timestamp)))
             data = np.frombuffer(ev.tobytes(), np.uint8)
             d_ev = torch.from_numpy(data.copy()).cuda() if len(data) else torch.zeros(128, dtype=torch.uint8).cuda()
             torch.cuda.synchronize()
             out.append(commit_general_batch(self.shards, self.summed, op, d_ev.data_ptr(), len(ev),
-                                            self.prepare_timestamp))
+                                            self.prepare_timestamp, auto_pulse=False))
         return out, False
 
-    def commit_window(self, op, batches, tick_ns=0):
-        """The five steps of csrc/shard.h with both exchanges summed in-process; returns the per-batch
-        replies assembled from every shard's home batches."""
+    def commit_window(self, op, batches, tick_ns=0, _pulsed=False):
+        """The harness pulse before the first batch when due, then the five steps of csrc/shard.h
+        with both exchanges summed in-process; returns the per-batch replies assembled from every
+        shard's home batches."""
         import torch
 
         self.prepare_timestamp += tick_ns
@@ -87,6 +108,10 @@ class LocalShards:
             self.prepare_timestamp += 1 + len(ev)
             ns.append(len(ev))
             ts.append(self.prepare_timestamp)
+        if not _pulsed and ts:
+            self.pulse_log.append((ts[0], self.pulse_before(ts[0])))
+        # no pulse is due at any later batch of the window (the device checks it too)
+        self.pulse_log.extend((t, self.shards[0].pulse(t)) for t in ts[1:])
         data = np.concatenate([np.frombuffer(ev.tobytes(), np.uint8) for ev in batches])
         d_ev = torch.from_numpy(data.copy()).cuda() if len(data) else torch.zeros(128, dtype=torch.uint8).cuda()
         torch.cuda.synchronize()

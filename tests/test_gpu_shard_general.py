@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from chaos import Chaos, run_protocol
-from oracle_sm import OracleStateMachine
+from oracle_sm import OracleStateMachine, lib as oracle_lib
 from test_gpu_shard import LocalShards, _compare_sharded
 from test_gpu_window import oracle_batches
 from tigerbeetle_amd import workload
@@ -27,6 +27,18 @@ def _statuses(sh):
     ts = np.concatenate([r[0] for r in rows])
     st = np.concatenate([r[1] for r in rows])
     return st[np.argsort(ts, kind="stable")]
+
+
+def oracle_logged(ref, op, batches, tick_ns, log):
+    """The restatement batch by batch under the harness protocol, logging (T, pulse()) before every
+    batch (state_machine.zig:589-596 at prepare_timestamp = T, before that batch's pulse)."""
+    out = []
+    for k, ev in enumerate(batches):
+        tick = tick_ns if k == 0 else 0
+        T = ref.prepare_timestamp + tick + 1 + len(ev)
+        log.append((T, bool(oracle_lib().tbo_pulse_needed(ref.h, T))))
+        out.append(run_protocol(ref, op, ev, tick))
+    return out
 
 
 def _check(sh, ref):
@@ -44,6 +56,7 @@ def test_shard_general_chaos(G, seed, win, bm):
     ref = OracleStateMachine(batch_max=bm)
     ch = Chaos(7000 + seed, n_accounts=30)
     fast = general = 0
+    ref_log = []
     try:
         for w in range(26):
             if w == 0 or w % 5 == 4:
@@ -58,13 +71,49 @@ def test_shard_general_chaos(G, seed, win, bm):
                 batches = [ch.transfers_batch(ch.rng.choice([1, 3, bm // 2, bm])) for _ in range(win)]
             tick = 0 if op == Operation.create_accounts else ch.rng.choice([0, 0, NS_PER_S, 2 * NS_PER_S])
             g, took_fast = sh.commit_any(op, batches, tick)
-            r = oracle_batches(ref, op, batches, tick)
+            r = oracle_logged(ref, op, batches, tick, ref_log)
             assert g == r, f"window {w} (fast={took_fast})"
+            # pulse() before every batch, the first one of the stream included (replica.zig:9459-9467)
+            assert sh.pulse_log == ref_log, f"window {w}"
             assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp(), f"window {w}"
             fast += int(took_fast)
             general += int(not took_fast)
         _check(sh, ref)
         assert fast > 0 and general > 0, (fast, general)
+    finally:
+        sh.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_shard_pulse_lockstep(G):
+    """pulse() on the shards equals the restatement's before every batch, from the very first one
+    (pulse_next_timestamp starts at timestamp_min on every engine, :2063): order-free account and
+    transfer windows, then two-phase batches with timeouts and ticks (pulses that expire, pulses that
+    expire nothing, and reset by post/void), then order-free windows again."""
+    bm = 16
+    sh = LocalShards(G, bm, 2048, 1 << 14, 4 * bm)
+    ref = OracleStateMachine(batch_max=bm)
+    ch = Chaos(7300 + G, n_accounts=20, pending=0.5, postvoid=0.3, limits=0.0, balancing=0.0, linked=0.1,
+               invalid=0.0)
+    ref_log = []
+    try:
+        assert sh.shards[0].pulse(1) and oracle_lib().tbo_pulse_needed(ref.h, 1)
+        plan = ([(Operation.create_accounts, [ch.accounts_batch(bm) for _ in range(2)], 0)] +
+                [(Operation.create_transfers, [workload.transfers_uniform(k * bm, bm, seed=5, n_accounts=20,
+                                                                          id_offset=100_000) for k in range(3)], 0)] +
+                [(Operation.create_transfers, [ch.transfers_batch(ch.rng.choice([1, bm // 2, bm]))],
+                  ch.rng.choice([0, NS_PER_S, 3 * NS_PER_S])) for _ in range(30)] +
+                [(Operation.create_transfers, [workload.transfers_uniform(k * bm, bm, seed=6, n_accounts=20,
+                                                                          id_offset=200_000) for k in range(3)], 70 * NS_PER_S)])
+        for w, (op, batches, tick) in enumerate(plan):
+            g, _ = sh.commit_any(op, batches, tick)
+            assert g == oracle_logged(ref, op, batches, tick, ref_log), f"window {w}"
+            assert sh.pulse_log == ref_log, f"window {w}"
+            assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp(), f"window {w}"
+        assert sum(p for _, p in ref_log) >= 3, ref_log
+        _check(sh, ref)
     finally:
         sh.close()
         ref.close()
@@ -125,9 +174,10 @@ def _rank_main(rank, world, port, seed, bm, out_dir):
 
     sh = ShardedStateMachine(world, rank, exchange_gloo, batch_max=bm, accounts_max=1024, transfers_max=1 << 14,
                              window_events_max=bm)
-    ts, replies = 0, []
+    ts, replies, pulses = 0, [], []
     for op, ev, tick in _dist_stream(seed, bm):
         ts += tick + 1 + len(ev)
+        pulses.append(sh.pulse(ts))  # pulse() before every batch, the first one included
         d_ev = torch.from_numpy(np.frombuffer(ev.tobytes(), np.uint8).copy()).cuda()
         torch.cuda.synchronize()
         replies.append(sh.commit_general(op, d_ev.data_ptr(), len(ev), ts).hex())
@@ -137,7 +187,7 @@ def _rank_main(rank, world, port, seed, bm, out_dir):
     import json
 
     with open(os.path.join(out_dir, f"rep{rank}.json"), "w") as f:
-        json.dump(replies, f)
+        json.dump({"replies": replies, "pulses": pulses}, f)
     sh.close()
     dist.destroy_process_group()
 
@@ -154,10 +204,14 @@ def test_shard_general_two_rank_gloo(tmp_path):
     mp.spawn(_rank_main, args=(world, _free_port(), seed, bm, str(tmp_path)), nprocs=world, join=True)
     ref = OracleStateMachine(batch_max=bm)
     try:
-        expect = [run_protocol(ref, op, ev, tick).hex() for op, ev, tick in _dist_stream(seed, bm)]
+        log = []
+        expect = [oracle_logged(ref, op, [ev], tick, log)[0].hex() for op, ev, tick in _dist_stream(seed, bm)]
         for r in range(world):
             with open(tmp_path / f"rep{r}.json") as f:
-                assert json.load(f) == expect
+                got = json.load(f)
+            assert got["replies"] == expect
+            assert got["pulses"] == [p for _, p in log]
+        assert log[0][1]  # the first pulse() is true
         acc = np.concatenate([np.load(tmp_path / f"acc{r}.npy") for r in range(world)])
         xfer = np.concatenate([np.load(tmp_path / f"xfer{r}.npy") for r in range(world)])
         st = np.concatenate([np.load(tmp_path / f"st{r}.npy") for r in range(world)])

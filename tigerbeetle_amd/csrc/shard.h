@@ -281,15 +281,15 @@ __global__ void __launch_bounds__(SEG) k_sh_roles(Dev d, Scratch s, const uint8_
 // The account owners need no validation: they read the account ids and the amount only (facts of an
 // event its home rejects statically are never read, and the commit bit gates every effect); every
 // amount they see counts toward the overflow bound, valid or not. Rewrites each entry's roles to the
-// A sharded window may hold several batches only if no pulse can fall due inside it. Sharded engines
-// never hold a pending transfer (outside the sharded class), so pulse_next stays timestamp_max and
-// only the one-second span can trip this; it is kept as a guard (window_error bit 3, tbg_sync
-// returns TBG_E_STATE).
+// A sharded window runs no pulse: the caller ran the harness pulse before its first batch when one
+// was due (through the general path), so no pulse may be due at any of its batches
+// (pulse_next > T_last), and a window of several batches spans less than a second. The class holds
+// no pending transfer, so the window itself cannot lower pulse_next. Kept as a guard (window_error
+// bit 3, tbg_sync returns TBG_E_STATE).
 __device__ inline void check_window(const WinDesc& w, Globals* g) {
-  if (w.nb <= 1) return;
   const uint64_t last = w.T[w.nb - 1];
   const uint64_t first_ts = win_ts(w, 0, w.off[0]);
-  if (last >= g->pulse_next || last >= first_ts + TB_NS_PER_S) atomicOr(&g->window_error, 8u);
+  if (last >= g->pulse_next || (w.nb > 1 && last >= first_ts + TB_NS_PER_S)) atomicOr(&g->window_error, 8u);
 }
 
 // ones that carry effects.

@@ -17,6 +17,13 @@ A window commits in five steps through the C ABI (include/tbg.h):
 
 The `exchange` callable is the only collective on the data path; with one shard there is none.
 Per shard, the work is the window's ids plus 1/G of the rest: it falls as G grows.
+
+pulse() (state_machine.zig:589-596) starts true on every shard (pulse_next_timestamp =
+timestamp_min, :2063), as on one engine. A pulse needs every shard's due expiry entries, so it runs
+through the general path (`pulse_general`): the due entries and their accounts are gathered, every
+shard expires the same ones, in the reference's (expires_at, timestamp) order and cap. A window goes
+through the five steps above only when no pulse is due at any of its batches (checked on the device:
+tbg_sync reports TBG_E_STATE otherwise).
 """
 import ctypes
 
@@ -96,6 +103,7 @@ class ShardedStateMachine:
         self.bits = torch.zeros(int(_lib.lib().tbg_shard_commit_bits_bytes(events_max)), dtype=torch.uint8, device=dev)
         self.stream = torch.cuda.ExternalStream(self.sm.stream, device=dev)
         self._n_events = 0
+        self._pulse_next = None  # cached pulse_next_timestamp (order-free windows never change it)
         torch.cuda.synchronize(device)
 
     @property
@@ -134,10 +142,14 @@ class ShardedStateMachine:
                    "shard_commit_window")
 
     def commit_window(self, operation, d_events, batch_events, batch_timestamps, d_results, d_batch_base):
-        """Asynchronous on the engine stream. Replies of this shard's home batches (home_range) land
-        in d_results / d_batch_base (d_batch_base[0..home_count]); returns (home_first, home_count)."""
+        """Asynchronous on the engine stream (after the harness pulse before the first batch, when
+        one is due: the general path, synchronous). Replies of this shard's home batches
+        (home_range) land in d_results / d_batch_base (d_batch_base[0..home_count]); returns
+        (home_first, home_count). No pulse may fall due at a later batch of the window."""
         import torch
 
+        if batch_timestamps and self.pulse(batch_timestamps[0]):
+            self.commit_pulse(batch_timestamps[0])  # the harness pulse before the first batch
         first, count = self.home_range(len(batch_events))
         words = self.prepare_window(operation, d_events, batch_events, batch_timestamps)
         if self.exchange is not None:
@@ -161,8 +173,26 @@ class ShardedStateMachine:
     # gathered read set by a scratch unsharded engine.
     # --------------------------------------------------------------------------------------------
     def pulse_next(self):
-        """pulse_next_timestamp, the same on every shard."""
-        return self.sm.stats()["pulse_next_timestamp"]
+        """pulse_next_timestamp, the same on every shard. Cached: an order-free window holds no
+        pending transfer and no timeout, so only the general path and pulses change it."""
+        if self._pulse_next is None:
+            self._pulse_next = self.sm.stats()["pulse_next_timestamp"]
+        return self._pulse_next
+
+    def pulse(self, prepare_timestamp):
+        """StateMachine.pulse() (state_machine.zig:589-596): pulse_next_timestamp <= prepare_timestamp."""
+        return self.pulse_next() <= prepare_timestamp
+
+    def commit_pulse(self, timestamp):
+        """commit(.pulse) at `timestamp` with this process's exchange (the replica logs one when
+        pulse() is true, vsr/replica.zig:9459-9487; the harness runs one before a batch at the
+        batch's timestamp, :2719-2739)."""
+        def summed(tensors):
+            if self.exchange is not None:
+                for t in tensors:
+                    self.exchange(t)
+
+        pulse_general([self], summed, timestamp)
 
     def _gx_init(self):
         import torch
@@ -199,9 +229,10 @@ class ShardedStateMachine:
 
         return commit_general_batch([self], summed, operation, d_events, n, timestamp)
 
-    def decide_apply(self, operation, d_events, n, timestamp):
-        """After both gathers were summed: the batch (and its pulse) on the scratch engine, then the
-        owned post-batch objects applied here. Returns the batch's reply bytes."""
+    def decide_apply(self, operation, d_events, n, timestamp, auto_pulse=True):
+        """After both gathers were summed: the batch (and its pulse when due, unless the caller
+        already ran it: auto_pulse False) on the scratch engine, then the owned post-batch objects
+        applied here. Returns the batch's reply bytes."""
         import torch
 
         from .state_machine import to_host
@@ -213,6 +244,7 @@ class ShardedStateMachine:
         def recs(off, count):
             return g[off: off + count * 128].view(count, 128)
 
+        pulse = int(operation) == int(Operation.pulse)
         xfer = int(operation) == int(Operation.create_transfers)
         accs = [recs(lay["ra"], 2 * n), recs(lay["rq"], 2 * G * C)]
         if xfer:
@@ -229,17 +261,21 @@ class ShardedStateMachine:
         _lib.check(L.tbg_open_device(sc.h, acc.data_ptr(), acc.shape[0], x.data_ptr(), xst.data_ptr(), x.shape[0], pn),
                    "open_device")
         sc.prepare_timestamp = timestamp
-        sc.commit_window(operation, d_events, [n], [timestamp], self.gx_res.data_ptr(), self.gx_base.data_ptr(),
-                         True, timestamp)
-        sc.sync()
-        base = to_host(self.gx_base)
-        reply = to_host(self.gx_res[: int(base[1]) * 8]).tobytes()
+        if pulse:  # commit(.pulse): the expiry runs whatever pulse_next says (:1874-1929)
+            reply = sc.commit(0, 0, timestamp, Operation.pulse, b"")
+        else:
+            sc.commit_window(operation, d_events, [n], [timestamp], self.gx_res.data_ptr(), self.gx_base.data_ptr(),
+                             auto_pulse, timestamp)
+            sc.sync()
+            base = to_host(self.gx_base)
+            reply = to_host(self.gx_res[: int(base[1]) * 8]).tobytes()
         pa, na, px, ps, nx, pn2 = (ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_void_p(),
                                    ctypes.c_uint64(), ctypes.c_uint64())
         _lib.check(L.tbg_device_state(sc.h, ctypes.byref(pa), ctypes.byref(na), ctypes.byref(px), ctypes.byref(ps),
                                       ctypes.byref(nx), ctypes.byref(pn2)), "device_state")
         _lib.check(L.tbg_shard_apply(self.sm.h, pa, na.value, px, ps, nx.value, pn2.value), "shard_apply")
         self.sm.sync()
+        self._pulse_next = pn2.value
         return reply
 
 
@@ -285,11 +321,27 @@ def _unique_by_timestamp(recs, status=None):
     return recs, status
 
 
-def commit_general_batch(shards, summed, operation, d_events, n, timestamp):
+def pulse_general(shards, summed, timestamp):
+    """commit(.pulse) at `timestamp` on `shards` (all shards in-process, or this process's one):
+    every shard offers its batch_max + 1 smallest due (expires_at, timestamp) entries and its
+    smallest live entry not yet due (gather 1), their accounts (gather 2); every shard then expires
+    the same global batch_max smallest on its scratch engine (:1010-1105, :1874-1929, :2018-2173) and
+    keeps what it owns."""
+    op = Operation.create_transfers  # the gather's layout for zero events: only the due rows
+    summed([s.gather(op, 0, 0, timestamp, 1) for s in shards])
+    summed([s.gather(op, 0, 0, timestamp, 2) for s in shards])
+    for s in shards:
+        s.decide_apply(Operation.pulse, 0, 0, timestamp)
+
+
+def commit_general_batch(shards, summed, operation, d_events, n, timestamp, auto_pulse=True):
     """One batch through the general path on `shards` (all shards in-process, or this process's
-    one); `summed(list of tensors)` sums them across all shards in place. Returns the reply."""
+    one); `summed(list of tensors)` sums them across all shards in place. With auto_pulse the
+    harness pulse before the batch runs with it when due; without, the caller ran it
+    (pulse_general: a capped pulse leaves pulse() true, and only one pulse precedes a batch).
+    Returns the reply."""
     summed([s.gather(operation, d_events, n, timestamp, 1) for s in shards])
     summed([s.gather(operation, d_events, n, timestamp, 2) for s in shards])
-    replies = [s.decide_apply(operation, d_events, n, timestamp) for s in shards]
+    replies = [s.decide_apply(operation, d_events, n, timestamp, auto_pulse) for s in shards]
     assert all(r == replies[0] for r in replies)
     return replies[0]

@@ -88,6 +88,10 @@ def main():
             ns.append(n)
             ts.append(prepare_ts)
         ptr = d_ev.data_ptr() + b0 * BATCH * 128
+        if shards[0].pulse(ts[0]):  # the harness pulse before the window (the first one only here)
+            from tigerbeetle_amd.sharding import pulse_general
+
+            pulse_general(shards, summed, ts[0])
         words, ev1 = timed_step(lambda r, s: s.prepare_window(op, ptr, ns, ts))
         summed(words)
         bits, ev2 = timed_step(lambda r, s: s.decide_window(*s.home_range(len(ns)), d_res.data_ptr(),
