@@ -50,20 +50,30 @@ PHASES = ["prep", "resolve", "classify", "wcount", "wlist", "walk", "final", "pu
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
 NS_PER_S = 1_000_000_000
 
-# Algorithmic bytes per event of each kernel (DESIGN.md §5 derives them).
-KERNEL_BYTES_PER_EVENT = {
-    # event read 128, two account-table entries 2x32, transfer-id probe 32, window key-map entry 16,
-    # per-event scratch written 72 (code, cls, batch, 4 slots/entries, amt, ...), the stamped record
-    # stored in place 128
-    "prep": 128 + 2 * 32 + 32 + 16 + 72 + 128,
-    # in-place records (every event inserted at its own rank): scratch read 40, two balance adds
-    # 2x64 (memory-side atomics), pending status 1, id read 16 + id-table entry 32
-    "final": 40 + 2 * 64 + 1 + 16 + 32,
+# Algorithmic bytes per window event of each phase: SURVEY §8(d)'s 640 B/event path (event read 128,
+# dr/cr account records 2 x 128, balance pairs written 2 x 32, transfer append 128, id keys 4 x 16)
+# split over the phases that move them; none of the engine's own scratch columns count.
+PHASE_ALG_BYTES = {
+    # event read 128, id keys: two account-id probes and the transfer-id probe 3 x 16, transfer
+    # record appended 128
+    "prep": 128 + 3 * 16 + 128,
+    # the dr/cr account records 2 x 128 and their balance pairs written 2 x 32, the transfer-id insert 16
+    "final": 2 * 128 + 2 * 32 + 16,
+    # the chunked resolver (balance-limit windows): per event side its amount 16 and its check bit
+    "resolve": 2 * (16 + 1),
 }
-# Windows that extend the sorted transfer prefix (ids strictly increasing above every stored id,
-# DESIGN.md §4): no transfer-id probe (the id is above every stored id), a direct 8 B key-map entry
-# instead of a claim, and no id read or id-table insert in k_final.
-KERNEL_BYTES_PER_EVENT_PREFIX = {"prep": 128 + 2 * 32 + 8 + 72 + 128, "final": 40 + 2 * 64 + 1}
+# the kernels each timed phase launches (the first is the one named in `roofline.kernel`)
+PHASE_KERNELS = {
+    "prep": ["k_ct_prep", "k_prep_reduce", "k_claim_fix", "k_bind_sum", "k_bind_decide", "k_bind_finish"],
+    "final": ["k_final<true>"],
+    "resolve": ["k_rc_run", "k_res_keys", "k_rc_build", "k_rc_sum", "k_res_apply", "k_res_final"],
+    "cpw": ["k_cc_walk<true>", "k_cc_init", "k_cc_link", "k_cc_keys", "onesweep sort", "k_cc_segs"],
+    "classify": ["k_classify<true>"], "wlist": ["k_wlist"], "walk": ["k_walk<true>", "k_wfold"],
+    "pulse": ["k_pulse", "k_xwin_rb", "k_xwin_minlive", "k_xwin_replay", "k_xwin_expire"],
+}
+# the walkers (cpw, walk) run the reference loop for the events they decide: event 128, balance
+# pairs 2 x 32, record 128 per walked event
+WALKED_EVENT_BYTES = 128 + 2 * 32 + 128
 
 CONFIGS = {
     "cfg1": dict(accounts=10_000, transfers=1_000_000, window=32, seed=42, tick=0),
@@ -85,7 +95,7 @@ def warm_phases(sm, nph):
     launches = (ctypes.c_uint64 * nph)()
     L.tbg_timing_collect(sm.h, ms, launches, nph)
     per_phase = {PHASES[p]: (ms[p] / launches[p] * 1000.0 if launches[p] else None) for p in range(nph)}
-    dom = max(("prep", "final"), key=lambda k: per_phase[k] or 0.0)
+    dom = max(PHASES, key=lambda k: per_phase[k] or 0.0)
     return per_phase, dom
 
 
@@ -95,7 +105,7 @@ def pmc_traffic(config, kernel, events_per_launch):
     FETCH_SIZE and WRITE_SIZE passes over the same bench command), scaled to this run's events per
     launch. Returns (raw FETCH+WRITE bytes, bytes with FETCH doubled per the gfx950 streaming-read
     correction, source) or None."""
-    for rnd in ("r2", "r1"):  # the latest round's summary of this config
+    for rnd in ("r3", "r2", "r1"):  # the latest round's summary of this config
         path = os.path.join(ROOT, "profiles", rnd, "pmc_%s.json" % config)
         if os.path.exists(path):
             break
@@ -136,6 +146,10 @@ def parse():
                    help="cfg1/cfg2: after the timed run, commit this many further transfers of the same stream "
                         "from pinned host memory (tbg_commit_window_host, H2D overlapped with compute) and report "
                         "it as `host_fed` (never `value`); default 8 windows, 0 = off")
+    p.add_argument("--id-order", default="sequential", choices=["sequential", "random", "reversed"],
+                   help="account and transfer ids as the reference benchmark's --id-order (cli.zig:97, 263-265; "
+                        "testing/id.zig IdPermutation; random = pseudo-UUIDs from Xoshiro256, the reference's own ids "
+                        "for the permutation seed DefaultPrng(seed) draws first)")
     p.add_argument("--change-log", action="store_true",
                    help="engine keeps the write-back change log (TBG_FLAG_CHANGE_LOG): its device cost")
     a = p.parse_args()
@@ -151,6 +165,10 @@ def parse():
     if a.host_fed_transfers is None:
         a.host_fed_transfers = 8 * min(a.window, WINDOW_BATCHES_MAX) * BATCH if a.config in ("cfg1", "cfg2") else 0
     a.tick = c["tick"]
+    from tigerbeetle_amd import workload
+
+    a.id_order_code = workload.ID_ORDERS[a.id_order]
+    a.perm_seed = workload.benchmark_permutation_seed(a.seed)
     return a
 
 
@@ -166,21 +184,25 @@ class HostStream:
     def n_accounts_total(self):
         return self.a.accounts + (CFG3_TREASURY if self.a.config == "cfg3" else 0)
 
+    def _ids(self, recs):
+        return self.w.permute_ids(recs, self.a.id_order_code, self.a.perm_seed)
+
     def accounts(self, first, count):
         if self.a.config == "cfg3":
-            return self.w.accounts_cfg3(first, count, self.seed, self.a.accounts, CFG3_TOP)
-        return self.w.accounts(first, count, self.seed)
+            return self._ids(self.w.accounts_cfg3(first, count, self.seed, self.a.accounts, CFG3_TOP))
+        return self._ids(self.w.accounts(first, count, self.seed))
 
     def funding(self, first, count):
-        return self.w.funding_cfg3(first, count, self.seed, self.a.accounts, CFG3_TREASURY, CFG3_FUND, CFG3_FUND_ID)
+        return self._ids(self.w.funding_cfg3(first, count, self.seed, self.a.accounts, CFG3_TREASURY, CFG3_FUND,
+                                             CFG3_FUND_ID))
 
     def transfers(self, first, count):
         a = self.a
         if a.config == "cfg3":
-            return self.w.transfers_zipf(first, count, self.seed, a.accounts, self.cdf)
+            return self._ids(self.w.transfers_zipf(first, count, self.seed, a.accounts, self.cdf))
         if a.config == "cfg4":
-            return self.w.transfers_cfg4(first, count, self.seed, a.accounts, BATCH)
-        return self.w.transfers_uniform(first, count, self.seed, a.accounts)
+            return self._ids(self.w.transfers_cfg4(first, count, self.seed, a.accounts, BATCH))
+        return self._ids(self.w.transfers_uniform(first, count, self.seed, a.accounts))
 
 
 def host_cpu():
@@ -214,6 +236,7 @@ def host_fed(args, sm, torch, first, n_acc, seed, win):
     d_tmp = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     _lib.check(L.tbg_gen_transfers_uniform(d_tmp.data_ptr(), first, n, seed, n_acc, 0, sm.stream), "gen")
+    _lib.check(L.tbg_gen_permute_ids(d_tmp.data_ptr(), n, 1, args.id_order_code, args.perm_seed, sm.stream), "ids")
     sm.sync()
     h_ev = torch.empty(n * 128, dtype=torch.uint8, pin_memory=True)
     h_ev.copy_(d_tmp)
@@ -353,6 +376,8 @@ def run_sharded(args, torch, dist, world, rank, device):
     torch.cuda.synchronize()
     _lib.check(L.tbg_gen_accounts(d_acc.data_ptr(), 0, n_acc, args.seed, 2, 1, 0, stream), "gen accounts")
     _lib.check(L.tbg_gen_transfers_uniform(d_xfer.data_ptr(), 0, n_xfer, args.seed, n_acc, 0, stream), "gen")
+    _lib.check(L.tbg_gen_permute_ids(d_acc.data_ptr(), n_acc, 0, args.id_order_code, args.perm_seed, stream), "ids")
+    _lib.check(L.tbg_gen_permute_ids(d_xfer.data_ptr(), n_xfer, 1, args.id_order_code, args.perm_seed, stream), "ids")
     sm.stream.synchronize()
 
     prepare_ts = 0
@@ -393,7 +418,8 @@ def run_sharded(args, torch, dist, world, rank, device):
         warm_windows.append(commit_range(Operation.create_transfers, d_xfer, b0, min(b0 + win, warm), n_xfer, widx))
         widx += 1
     sm.sync()
-    per_phase, dom = warm_phases(sm, NPH)
+    per_phase, _ = warm_phases(sm, NPH)
+    dom = max(("prep", "final"), key=lambda k: per_phase[k] or 0.0)  # the owned-work and apply kernels
     # timed region: only the roofline kernel's phase records events (two per window)
     L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else (1 << PHASES.index(dom)))
     barrier()
@@ -465,6 +491,7 @@ def run_sharded(args, torch, dist, world, rank, device):
             "config": {"workload": "cfg5: %d accounts hash-sharded over %d GPU(s), %d uniform create_transfers "
                                    "(%.1f %% cross-shard), %d/batch" % (n_acc, G, n_xfer, 100.0 * (G - 1) / G, BATCH),
                        "batch": BATCH, "window_batches": win, "accounts_per_gpu": args.accounts,
+                       "id_order": args.id_order,
                        "transfers_per_gpu": args.transfers,
                        "parallelism": "hash-sharded accounts+ids, home batch ranges, two RCCL all-reduces "
                                       "per window (owner facts, commit bits)" if G > 1 else "single shard"},
@@ -577,6 +604,9 @@ def main():
             _lib.check(L.tbg_gen_transfers_cfg4(d_xfer.data_ptr(), 0, n_xfer, seed, n_acc, BATCH, 0, stream), "gen")
         else:
             _lib.check(L.tbg_gen_transfers_uniform(d_xfer.data_ptr(), 0, n_xfer, seed, n_acc, 0, stream), "gen")
+    # --id-order: one bijection over every generated id (accounts, funding, transfers)
+    for d, n, kind in ((d_acc, n_acc_total, 0), (d_setup, n_setup, 1), (d_xfer, n_xfer, 1)):
+        _lib.check(L.tbg_gen_permute_ids(d.data_ptr(), n, kind, args.id_order_code, args.perm_seed, stream), "ids")
 
     prepare_ts = 0
 
@@ -621,7 +651,8 @@ def main():
         widx += 1
     _lib.check(L.tbg_sync(sm.h), "sync (warmup)")
     per_phase, dom = warm_phases(sm, NPH)
-    walker_before = sm.stats()["walker_events"]
+    stats_before = sm.stats()
+    walker_before = stats_before["walker_events"]
     if dist:
         dist.barrier()
     # timed region: only the roofline kernel's phase records events (two per window)
@@ -681,18 +712,28 @@ def main():
             us = ms[di] / launches[di] * 1000.0
             ev_per_launch = timed_events / launches[di]
             prefix = stats["sorted_transfers"] == stats["transfers"]  # every window extended the prefix
-            per_event = (KERNEL_BYTES_PER_EVENT_PREFIX if prefix else KERNEL_BYTES_PER_EVENT)[dom]
-            bytes_launch = int(per_event * ev_per_launch)
-            achieved = bytes_launch / (us * 1e-6) / 1e9
-            kname = {"prep": "k_ct_prep", "final": "k_final<true>"}[dom]
-            tr = pmc_traffic(cfg, kname, ev_per_launch)
-            roof = {"bound": "hbm", "kernel": kname, "events_per_launch": int(ev_per_launch),
-                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
-                    "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
-                    "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch, "alg_bytes_per_event": per_event, "sorted_prefix": prefix,
+            if dom in ("cpw", "walk"):
+                key = "component_events" if dom == "cpw" else "walker_events"
+                walked = stats[key] - stats_before[key]
+                per_event = WALKED_EVENT_BYTES * walked / max(timed_events, 1)
+            else:
+                per_event = PHASE_ALG_BYTES.get(dom)
+            kname = PHASE_KERNELS[dom][0]
+            roof = {"bound": "hbm", "kernel": kname, "phase": dom, "phase_kernels": PHASE_KERNELS[dom],
+                    "events_per_launch": int(ev_per_launch), "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": None, "traffic": None, "avg_launch_us": round(us, 2), "alg_bytes_per_event": per_event,
+                    "alg_bytes_basis": "SURVEY 8(d) 640 B/event path split over the phases (bench.py PHASE_ALG_BYTES); "
+                                       "no scratch columns", "sorted_prefix": prefix,
                     "phase_avg_us_warmup": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
-                    "path_alg_GBs": round(640 * all_events / elapsed / 1e9 / max(world, 1), 1)}
+                    "path_alg_GBs": round(640 * all_events / elapsed / 1e9 / max(world, 1), 1),
+                    "path_frac": round(640 * all_events / elapsed / 1e9 / max(world, 1) / HBM_PEAK_GBS, 4)}
+            if per_event:
+                bytes_launch = int(per_event * ev_per_launch)
+                achieved = bytes_launch / (us * 1e-6) / 1e9
+                tr = pmc_traffic(cfg, kname, ev_per_launch)
+                roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                             "alg_bytes_per_launch": bytes_launch, "traffic": tr[0] if tr else None,
+                             "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None})
         desc = {
             "cfg1": "cfg1: %d accounts, %d uniform create_transfers, %d/batch",
             "cfg2": "cfg2: %d accounts, %d uniform create_transfers (no flags), %d/batch",
@@ -714,6 +755,7 @@ def main():
             "dtype": "u128",
             "data": "synthetic (device-generated, seed %d)" % args.seed,
             "config": {"workload": desc, "batch": BATCH, "window_batches": win, "accounts_per_gpu": n_acc,
+                       "id_order": args.id_order,
                        "transfers_per_gpu": n_xfer, "resolver": args.resolver, "change_log": bool(args.change_log),
                        "parallelism": "independent databases, one per rank (not sharded)" if world > 1 else "single GPU"},
             "results": {"failed_events_timed": int(all_fails),

@@ -89,7 +89,9 @@ int tbg_prefetch(tbg_engine *engine, uint64_t op, uint32_t operation, const void
  * get_account_balances (input: one tb_account_filter_t; reply: Transfer / AccountBalance records,
  * :1346-1419). Writes exactly the reply bytes the reference writes into `output` (for create_*:
  * packed {u32 index, u32 result} for non-ok events, ascending index) and the byte count into
- * *output_len. Synchronous. Queries run on unsharded engines (TBG_E_STATE on a shard). */
+ * *output_len. Synchronous. On a shard: pulses go through the general path (pulse_general in
+ * tigerbeetle_amd/sharding.py), lookups and queries through tbg_shard_lookup / tbg_shard_query
+ * (TBG_E_STATE here). */
 int tbg_commit(tbg_engine *engine, uint64_t op, uint64_t timestamp, uint32_t operation, const void *input,
                uint64_t input_len, void *output, uint64_t output_cap, uint64_t *output_len);
 
@@ -178,7 +180,9 @@ int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, const vo
  * object trees are keyed by timestamp) and, per transfer, its TransferPending status (0 none,
  * 1 pending, 2 posted, 3 voided, 4 expired; NULL = all 0), and the account_balances groove's rows
  * (historical_balance, :1806-1841; sorted by timestamp). pulse_next_timestamp starts at
- * timestamp_min, as in a freshly initialised StateMachine (:2063). TBG_E_STATE if not empty. */
+ * timestamp_min, as in a freshly initialised StateMachine (:2063). TBG_E_STATE if not empty. A shard
+ * is handed the same whole set and keeps what it owns (accounts and transfers by tbg_shard_of(id); a
+ * status and a history row go with their transfer). */
 int tbg_open(tbg_engine *engine, const tb_account_t *accounts, uint64_t n_accounts, const tb_transfer_t *transfers,
              uint64_t n_transfers, const uint8_t *pending_status,
              const tb_account_balances_value_t *account_balances, uint64_t n_account_balances);
@@ -274,9 +278,32 @@ int tbg_aof_replay(tbg_engine *engine, const void *h_aof, uint64_t size, uint32_
 uint64_t tbg_shard_gather_bytes(uint32_t n_events, uint32_t shard_count, uint32_t batch_max, uint64_t *phase2_offset);
 int tbg_shard_gather(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_events,
                      uint64_t timestamp, uint32_t phase, void *d_buffer);
+/* d_history / d_history_side (tbg_device_history of the scratch engine, may be NULL): the history
+ * row beside each of d_transfers, kept with the transfers this shard inserts. With
+ * TBG_FLAG_CHANGE_LOG the shard's write-back stream (tbg_window_changes) then lists what changed on
+ * this shard: updated accounts, inserted records, TransferPending rows. */
 int tbg_shard_apply(tbg_engine *engine, const tb_account_t *d_accounts, uint64_t n_accounts,
                     const tb_transfer_t *d_transfers, const uint8_t *d_status, uint64_t n_transfers,
-                    uint64_t pulse_next_timestamp);
+                    const void *d_history, const uint8_t *d_history_side, uint64_t pulse_next_timestamp);
+
+/* Reads on a sharded engine (tigerbeetle_amd/csrc/shard_read.inc): every shard gets the same request
+ * body and writes what it owns into its part of a device buffer; the caller sums the buffer
+ * byte-wise across the shards in place (the same uint8 all-reduce as the commit path; one writer per
+ * byte); then any shard builds the reply, byte-identical to an unsharded engine's tbg_commit reply.
+ *   lookup_accounts / lookup_transfers (state_machine.zig:1309-1344): tbg_shard_lookup_bytes(n ids),
+ *     tbg_shard_lookup (asynchronous), sum, tbg_shard_lookup_reply (synchronous);
+ *   get_account_transfers / get_account_balances (:786-996, 1346-1419):
+ *     tbg_shard_query_bytes(shard_count, batch_max), tbg_shard_query (synchronous: each shard's
+ *     first min(limit, batch_max) matches in scan order, with their history rows), sum,
+ *     tbg_shard_query_merge (the regions merged by timestamp in scan order, cut at the limit). */
+uint64_t tbg_shard_lookup_bytes(uint32_t n_ids);
+int tbg_shard_lookup(tbg_engine *engine, uint32_t operation, const void *input, uint64_t input_len, void *d_buffer);
+int tbg_shard_lookup_reply(tbg_engine *engine, const void *d_buffer, uint64_t input_len, void *output,
+                           uint64_t output_cap, uint64_t *output_len);
+uint64_t tbg_shard_query_bytes(uint32_t shard_count, uint32_t batch_max);
+int tbg_shard_query(tbg_engine *engine, uint32_t operation, const void *filter, uint64_t filter_len, void *d_buffer);
+int tbg_shard_query_merge(tbg_engine *engine, uint32_t operation, const void *filter, const void *d_buffer,
+                          void *output, uint64_t output_cap, uint64_t *output_len);
 /* Unsharded engines: open (as tbg_open) from device-resident objects in timestamp order with the
  * given pulse_next_timestamp; and the device view of the whole state (valid until the next call
  * that changes it). */
@@ -286,6 +313,10 @@ int tbg_open_device(tbg_engine *engine, const tb_account_t *d_accounts, uint64_t
 int tbg_device_state(tbg_engine *engine, const tb_account_t **accounts, uint64_t *n_accounts,
                      const tb_transfer_t **transfers, const uint8_t **status, uint64_t *n_transfers,
                      uint64_t *pulse_next_timestamp);
+/* The history rows beside those transfer records (128 B per slot: the debit then the credit
+ * account's four balances after the transfer) and per slot the sides present (bit 0 debit, bit 1
+ * credit). */
+int tbg_device_history(tbg_engine *engine, const void **rows, const uint8_t **sides);
 
 /* Test hook mirroring the harness `setup` action (state_machine.zig:2545-2561). */
 int tbg_setup_balances(tbg_engine *engine, const tb_uint128_t *id, const tb_uint128_t *debits_pending,
@@ -314,7 +345,8 @@ int tbg_debug_counters(tbg_engine *engine, uint64_t *out, uint32_t n);
  * window: every account record whose balances they changed (current values, ascending creation
  * order) followed by the accounts the window created, every transfer record it inserted (commit
  * order), and the TransferPending rows inserted or updated (new pending transfers, earlier ones
- * posted, voided or expired; ascending timestamp). Unsharded engines. Synchronous.
+ * posted, voided or expired; ascending timestamp). On a shard: what changed among the objects it owns
+ * (an order-free window, or the general path's tbg_shard_apply). Synchronous.
  * TBG_E_CAPACITY if a buffer is too small (the counts are still written); TBG_E_STATE without the
  * flag. */
 int tbg_window_changes(tbg_engine *engine, tb_account_t *accounts, uint64_t accounts_cap, uint64_t *accounts_count,
@@ -332,6 +364,13 @@ int tbg_device_stores(tbg_engine *engine, const tb_account_t **accounts, const t
 /* Synthetic request streams generated directly in HBM (tigerbeetle_amd/csrc/workload.hip),
  * shaped like the reference benchmark (src/tigerbeetle/benchmark_load.zig:206-327). `stream` is a
  * hipStream_t (e.g. tbg_stream(engine)). Bit-identical to tigerbeetle_amd/workload.py. */
+/* Id orders of `tigerbeetle benchmark --id-order` (cli.zig:97, 263-265; testing/id.zig:8-48): rewrite,
+ * in place, the sequential ids (data = index + 1) of `count` generated records in HBM as
+ * IdPermutation.encode(data): order 0 sequential, 1 random (pseudo-UUID from Xoshiro256(seed +% data),
+ * the reference's own ids for permutation seed `seed`), 2 reversed (maxInt(u128) - data). Accounts: the
+ * id; transfers (`transfers` = 1): the id, both account ids and pending_id (0 and ids >= 2^64 stay). */
+int tbg_gen_permute_ids(void *d_records, uint64_t count, uint32_t transfers, uint32_t order, uint64_t seed,
+                        void *stream);
 int tbg_gen_accounts(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint32_t ledger, uint16_t code,
                      uint16_t flags, void *stream);
 int tbg_gen_transfers_uniform(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,

@@ -38,33 +38,40 @@ def _check_digest(gpu, ref):
     assert gpu.digest() == want
 
 
-def _accounts(gpu, ref, seed):
-    acc = _batches(workload.accounts(0, N_ACC, seed))
+def _accounts(gpu, ref, seed, order=0, perm_seed=0):
+    acc = _batches(workload.permute_ids(workload.accounts(0, N_ACC, seed), order, perm_seed))
     for w0 in range(0, len(acc), 128):
         assert commit_window(gpu, Operation.create_accounts, acc[w0:w0 + 128]) == \
             oracle_batches(ref, Operation.create_accounts, acc[w0:w0 + 128])
 
 
 @pytest.mark.gpu
-def test_geometry_cfg2_uniform():
-    """bench.py's cfg2 path: device-generated stream, tbg_commit_window over 128 batches."""
+@pytest.mark.parametrize("id_order", ["sequential", "random", "reversed"])
+def test_geometry_cfg2_uniform(id_order):
+    """bench.py's cfg2 path: device-generated stream, tbg_commit_window over 128 batches; with
+    `bench.py --id-order` random / reversed (the reference benchmark's IdPermutation, cli.zig:263-265)
+    every account and transfer id is permuted, so the windows take the hashed id path (no sorted
+    prefix, key-map claims)."""
     import torch
 
     from tigerbeetle_amd import StateMachine, _lib
 
     L = _lib.lib()
     n_win, seed = 3, 44
+    order = workload.ID_ORDERS[id_order]
+    perm_seed = workload.benchmark_permutation_seed(seed)
     n_x = n_win * 128 * BM
     gpu = StateMachine(batch_max=BM, accounts_max=N_ACC, transfers_max=n_x, window_events_max=128 * BM)
     ref = OracleStateMachine(batch_max=BM)
     try:
-        _accounts(gpu, ref, seed)
+        _accounts(gpu, ref, seed, order, perm_seed)
         d_x = torch.empty(n_x * 128, dtype=torch.uint8, device="cuda")
         d_res = torch.zeros(128 * BM * 8, dtype=torch.uint8, device="cuda")
         d_base = torch.zeros(129, dtype=torch.int32, device="cuda")
         torch.cuda.synchronize()
         _lib.check(L.tbg_gen_transfers_uniform(d_x.data_ptr(), 0, n_x, seed, N_ACC, 0, gpu.stream), "gen")
-        host = workload.transfers_uniform(0, n_x, seed, N_ACC)
+        _lib.check(L.tbg_gen_permute_ids(d_x.data_ptr(), n_x, 1, order, perm_seed, gpu.stream), "permute")
+        host = workload.permute_ids(workload.transfers_uniform(0, n_x, seed, N_ACC), order, perm_seed)
         for w in range(n_win):
             ns, ts = [], []
             for _ in range(128):
@@ -78,7 +85,9 @@ def test_geometry_cfg2_uniform():
             res = to_host(d_res).tobytes()
             r = oracle_batches(ref, Operation.create_transfers, _batches(host, w * 128 * BM, 128 * BM))
             assert [res[base[b] * 8: base[b + 1] * 8] for b in range(128)] == r
-        assert gpu.stats()["transfers"] == n_x
+        st = gpu.stats()
+        assert st["transfers"] == n_x
+        assert (st["sorted_transfers"] == n_x) == (id_order == "sequential")
         _check_digest(gpu, ref)
         _compare_final(gpu, ref)
     finally:

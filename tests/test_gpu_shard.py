@@ -19,14 +19,23 @@ BM = 8190
 class LocalShards:
     """G shards of one engine on cuda:0, driven like one StateMachine (harness timestamps)."""
 
-    def __init__(self, G, batch_max, accounts_max, transfers_max, window_events_max):
+    def __init__(self, G, batch_max, accounts_max, transfers_max, window_events_max, change_log=False):
         from tigerbeetle_amd.sharding import ShardedStateMachine
 
         self.shards = [ShardedStateMachine(G, r, None, batch_max=batch_max, accounts_max=accounts_max,
-                                           transfers_max=transfers_max, window_events_max=window_events_max)
+                                           transfers_max=transfers_max, window_events_max=window_events_max,
+                                           change_log=change_log)
                        for r in range(G)]
         self.prepare_timestamp = 0
         self.pulse_log = []  # (T, pulse()) before every batch, the harness order (:2719-2739)
+        # with change_log: every commit call's write-back stream per shard, drained after each call
+        # (a replica hands each one to its forest): lists of (shard, accounts, transfers, rows)
+        self.logs = [] if change_log else None
+
+    def _drain(self):
+        if self.logs is not None:
+            for r, s in enumerate(self.shards):
+                self.logs.append((r,) + tuple(s.window_changes()))
 
     def close(self):
         for s in self.shards:
@@ -54,6 +63,7 @@ class LocalShards:
         assert all(s.pulse(T) == due for s in self.shards)
         if due:
             pulse_general(self.shards, self.summed, T)
+            self._drain()
         return due
 
     def commit_any(self, op, batches, tick_ns=0):
@@ -94,6 +104,7 @@ class LocalShards:
             torch.cuda.synchronize()
             out.append(commit_general_batch(self.shards, self.summed, op, d_ev.data_ptr(), len(ev),
                                             self.prepare_timestamp, auto_pulse=False))
+            self._drain()
         return out, False
 
     def commit_window(self, op, batches, tick_ns=0, _pulsed=False):
@@ -131,6 +142,7 @@ class LocalShards:
             s.commit_decided()
         for s in self.shards:
             s.sync()
+        self._drain()
         replies = [None] * len(ns)
         for first, count, d_res, d_base in outs:
             res = to_host(d_res).tobytes()
@@ -139,6 +151,12 @@ class LocalShards:
                 replies[first + k] = res[base[k] * 8: base[k + 1] * 8]
         assert all(r is not None for r in replies)
         return replies
+
+    def read(self, op, data):
+        """A lookup or query, gathered from the owners (csrc/shard_read.inc)."""
+        from tigerbeetle_amd.sharding import read_general
+
+        return read_general(self.shards, self.summed, op, data)
 
     def dump_accounts(self):
         a = np.concatenate([s.sm.dump_accounts() for s in self.shards])
@@ -306,7 +324,7 @@ def test_shard_mixed_results(G, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["pending", "duplicate", "limit", "post", "balancing"])
+@pytest.mark.parametrize("kind", ["pending", "duplicate", "limit", "post", "balancing", "history"])
 def test_shard_rejects_windows_outside_class(kind):
     """Windows outside the sharded class fail with TBG_E_UNSUPPORTED and change nothing anywhere."""
     from tigerbeetle_amd._lib import UnsupportedWindow
@@ -314,8 +332,9 @@ def test_shard_rejects_windows_outside_class(kind):
     G, n_acc = 2, 64
     sh = LocalShards(G, 64, 1024, 4096, 256)
     try:
-        a = workload.accounts(0, n_acc, seed=3)
+        a = workload.accounts(0, n_acc + 1, seed=3)
         a["flags"][5] = 2  # account 6: debits_must_not_exceed_credits
+        a["flags"][n_acc] = 8  # account 65 (outside the uniform stream): flags.history
         sh.commit_window(Operation.create_accounts, [a])
         t = workload.transfers_uniform(0, 40, seed=3, n_accounts=n_acc)
         t["debit_account_id_lo"] = np.where(t["debit_account_id_lo"] == 6, 7, t["debit_account_id_lo"])
@@ -333,6 +352,9 @@ def test_shard_rejects_windows_outside_class(kind):
             bad["id_lo"][7] = bad["id_lo"][2]
         elif kind == "limit":
             bad["debit_account_id_lo"][4] = 6
+            bad["credit_account_id_lo"][4] = 12
+        elif kind == "history":  # a historical_balance row (state_machine.zig:1806-1841)
+            bad["debit_account_id_lo"][4] = n_acc + 1
             bad["credit_account_id_lo"][4] = 12
         elif kind == "post":
             bad["flags"][5] = 4

@@ -13,7 +13,7 @@ EXPORTS = [
     "tbg_create", "tbg_destroy", "tbg_input_valid", "tbg_pulse_needed", "tbg_prefetch", "tbg_commit",
     "tbg_commit_device", "tbg_commit_window", "tbg_sync", "tbg_stream", "tbg_setup_balances", "tbg_get_stats",
     "tbg_dump_accounts", "tbg_dump_transfers", "tbg_dump_transfer_status", "tbg_device_stores",
-    "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_version", "tbg_debug_last_batch",
+    "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_gen_permute_ids", "tbg_version", "tbg_debug_last_batch",
     "tbg_timing_enable", "tbg_timing_collect", "tbg_gen_accounts_cfg3", "tbg_gen_funding_cfg3",
     "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4", "tbg_debug_counters", "tbg_shard_of",
     "tbg_shard_prepare_window", "tbg_shard_decide_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
@@ -21,7 +21,8 @@ EXPORTS = [
     "tbg_open", "tbg_reset", "tbg_prefetch_poll", "tbg_compact", "tbg_checkpoint", "tbg_digest",
     "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free", "tbg_checksum",
     "tbg_demux_init", "tbg_demux_decode", "tbg_aof_replay", "tbg_shard_gather_bytes", "tbg_shard_gather",
-    "tbg_shard_apply", "tbg_open_device", "tbg_device_state",
+    "tbg_shard_apply", "tbg_open_device", "tbg_device_state", "tbg_device_history", "tbg_shard_lookup_bytes",
+    "tbg_shard_lookup", "tbg_shard_lookup_reply", "tbg_shard_query_bytes", "tbg_shard_query", "tbg_shard_query_merge",
 ]
 
 
@@ -110,6 +111,7 @@ def lib():
         "tbg_device_stores": ([vp, P(vp), P(vp)], i32),
         "tbg_gen_accounts": ([vp, u64, u64, u64, u32, ctypes.c_uint16, ctypes.c_uint16, vp], i32),
         "tbg_gen_transfers_uniform": ([vp, u64, u64, u64, u64, u64, vp], i32),
+        "tbg_gen_permute_ids": ([vp, u64, u32, u32, u64, vp], i32),
         "tbg_version": ([], ctypes.c_char_p),
         "tbg_debug_last_batch": ([vp, vp, vp, u32], i32),
         "tbg_timing_enable": ([vp, ctypes.c_int], i32),
@@ -143,7 +145,14 @@ def lib():
         "tbg_aof_replay": ([vp, vp, u64, u32, P(AofStats)], i32),
         "tbg_shard_gather_bytes": ([u32, u32, u32, P(u64)], u64),
         "tbg_shard_gather": ([vp, u32, vp, u32, u64, u32, vp], i32),
-        "tbg_shard_apply": ([vp, vp, u64, vp, vp, u64, u64], i32),
+        "tbg_shard_apply": ([vp, vp, u64, vp, vp, u64, vp, vp, u64], i32),
+        "tbg_device_history": ([vp, P(vp), P(vp)], i32),
+        "tbg_shard_lookup_bytes": ([u32], u64),
+        "tbg_shard_lookup": ([vp, u32, vp, u64, vp], i32),
+        "tbg_shard_lookup_reply": ([vp, vp, u64, vp, u64, P(u64)], i32),
+        "tbg_shard_query_bytes": ([u32, u32], u64),
+        "tbg_shard_query": ([vp, u32, vp, u64, vp], i32),
+        "tbg_shard_query_merge": ([vp, u32, vp, vp, vp, u64, P(u64)], i32),
         "tbg_open_device": ([vp, vp, u64, vp, vp, u64, u64], i32),
         "tbg_device_state": ([vp, P(vp), P(u64), P(vp), P(vp), P(u64), P(u64)], i32),
     }

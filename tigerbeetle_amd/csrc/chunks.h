@@ -33,6 +33,10 @@
 #define RC_EM_IDX 0x7FFu
 #define RC_EM_CHECK 0x800u
 #define RC_EM_ADD 0x1000u
+#ifndef RC_HEAD_SIMD
+#define RC_HEAD_SIMD 1  // 1: the chunk's longest segment walked by wave 0 alone on its SIMD; 2: by wave 0
+                        // (others share the SIMD); 0: taken from the long queue like any other
+#endif
 #ifndef RC_PROF
 #define RC_PROF 0  // 1: per-phase clock64() sums of k_rc_run into Globals::dbg (tbg_debug_counters)
 #endif
@@ -485,6 +489,19 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
     __syncthreads();
     RC_ADD(0, tp0);
     const uint32_t nshort = nseg - nlong;
+    // The chunk's longest segment (the Zipf head's: the iteration's critical path) is walked by wave
+    // 0 with its SIMD to itself: the other waves of that SIMD (waves 4, 8, 12; waves go to SIMDs
+    // round-robin) sit the walk phase out, so the head's steps do not share issue slots.
+    uint32_t H = RC_NONE, hlen = 0;
+    for (uint32_t j = 0; RC_HEAD_SIMD && j < nhuge; j++) {
+      const uint32_t sg = rc_uniform(L.lst[j]);
+      const uint32_t len = rc_uniform(L.seg[sg + 1]) - rc_uniform(L.seg[sg]);
+      if (len > hlen) {
+        hlen = len;
+        H = sg;
+      }
+    }
+    const uint32_t wv = t >> 6;
     for (uint32_t it = 0;; it++) {
       if (it > RC_C + 1) {  // cannot happen (see header); the sequential walker takes the window
         if (t == 0) g->res_error = 1;
@@ -497,10 +514,22 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
       // compiler's wave aggregation): the long queue counts 64 per grab, the short queue hands each
       // lane its own index. No lane-divergent branch around the atomic, so the loops stay
       // wave-uniform (a grab under `if (lane == 0)` let the compiler split the loop per lane).
-      for (;;) {
+      if (H != RC_NONE && wv == 0) {
+        const uint32_t kf = rc_uniform(L.dfrom[H]);
+        if (kf != RC_NONE) {
+          L.dfrom[H] = RC_NONE;
+          __builtin_amdgcn_s_setprio(3);
+          if (big) rc_walk_wave(L, H, kf, lane);
+          else rc_walk_wave32(L, H, kf, lane, wrounds, wt);
+          __builtin_amdgcn_s_setprio(0);
+        }
+      }
+      const bool sit_out = RC_HEAD_SIMD == 1 && H != RC_NONE && wv != 0 && (wv & 3u) == 0;
+      for (; !sit_out;) {
         const uint32_t j = rc_uniform(atomicAdd(&L.qlong, 1u)) >> 6;
         if (j >= nlong) break;
         const uint32_t sg = rc_uniform(L.lst[j]);
+        if (sg == H) continue;
         const uint32_t kf = rc_uniform(L.dfrom[sg]);
         if (kf == RC_NONE) continue;
         L.dfrom[sg] = RC_NONE;
@@ -520,7 +549,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
           }
         }
       }
-      for (;;) {
+      for (; !sit_out;) {
         const uint32_t j = atomicAdd(&L.qshort, 1u);
         if (rc_uniform(j) >= nshort) break;
         if (j < nshort) {

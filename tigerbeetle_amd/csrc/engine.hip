@@ -1656,3 +1656,4 @@ __global__ void k_setup(Dev d, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dp
 #include "host.inc"
 #include "aof.inc"
 #include "shard_gx.inc"
+#include "shard_read.inc"

@@ -27,12 +27,14 @@
 //                 the amounts (exact 128-bit atomics) and the id owner appends the record.
 //
 // The sharded class is the order-free one: no balance read (no limit flag on a touched
-// account, no balancing), no two-phase, no in-window duplicate id, overflow-free window. Then every
+// account, no balancing), no history row (no flags.history on a touched account), no two-phase, no
+// in-window duplicate id, overflow-free window. Then every
 // event's outcome is a function of the owners' facts alone, and the effects commute. A window outside
 // the class is detected before anything is applied (by an owner: exchange 1's trailer; by a home:
 // exchange 2's trailer), so every shard reaches the same verdict and the window fails with
 // TBG_E_UNSUPPORTED at tbg_sync: no shard applies any of it.
 #pragma once
+#include "changes.h"
 #include "sm_logic.h"
 #include "walker.h"
 #include "window.h"
@@ -45,8 +47,9 @@
 //   [16, 16+4E)     debit account's ledger (its owner; 0 = not found: a live ledger is never 0, :1436)
 //   [16+4E, 16+8E)  credit account's ledger
 //   [16+8E, 16+9E)  bits 0-5: 1 + (TB_CT_OK or the exists* code), by the transfer-id owner;
-//                   bit 6: the debit account has debits_must_not_exceed_credits (its owner);
-//                   bit 7: the credit account has credits_must_not_exceed_debits (its owner)
+//                   bit 6: the debit account has debits_must_not_exceed_credits or flags.history
+//                   (its owner); bit 7: the credit account has credits_must_not_exceed_debits or
+//                   flags.history (its owner)
 //   create_accounts:
 //   [16, 16+E)      bits 0-5: 1 + the id owner's code
 enum : uint32_t { SH_Z_MASK = 0x3F, SH_DR_LIMIT = 0x40, SH_CR_LIMIT = 0x80 };
@@ -347,7 +350,9 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
         uint32_t drl = 0;
         if (slot != NONE32) {
           drl = e.ledger;
-          if (e.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) zw |= SH_DR_LIMIT;
+          // a limit (a balance read) or flags.history (a historical_balance row of balances after
+          // the event, :1806-1841): outside the order-free class if the event commits
+          if (e.flags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS | TB_ACCOUNT_HISTORY)) zw |= SH_DR_LIMIT;
         }
         xch.drl[i] = drl;
       }
@@ -359,7 +364,7 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
         uint32_t crl = 0;
         if (slot != NONE32) {
           crl = e.ledger;
-          if (e.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) zw |= SH_CR_LIMIT;
+          if (e.flags & (TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS | TB_ACCOUNT_HISTORY)) zw |= SH_CR_LIMIT;
         }
         xch.crl[i] = crl;
       }
@@ -464,7 +469,8 @@ __device__ inline uint32_t sh_code(const Scratch& s, const uint8_t* ev, const Xc
     return TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
   if (z != TB_CT_OK) return z;  // exists* (:1506-1507)
   // Reaches the balance checks: overflow cannot fail in a class window; a limit flag on either
-  // account is a balance read (:1546-1547), outside the class.
+  // account is a balance read (:1546-1547), and flags.history a row of balances after the event
+  // (:1806-1841): outside the class.
   if (zw & (SH_DR_LIMIT | SH_CR_LIMIT)) atomicOr(&trailer2[0], 1u);
   return TB_CT_OK;
 }
@@ -580,7 +586,7 @@ __global__ void __launch_bounds__(SEG) k_sh_icount(Dev d, Scratch s, uint32_t xf
 template <bool XFER>
 __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w,
                                                   const uint32_t* trailer1, const uint32_t* trailer2,
-                                                  const unsigned long long* bits) {
+                                                  const unsigned long long* bits, ChgLog chg, uint32_t chg_epoch) {
   __shared__ uint32_t lds[SEG / 64];
   __shared__ unsigned long long ldsm[SEG / 64];
   // inserted transfer records, compacted per wave and stored as one contiguous run (as in k_final)
@@ -624,6 +630,10 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
       Add128 a_dr, a_cr;
       if (drs != NONE32) a_dr.issue(&d.acc[drs].debits_posted, a, small);
       if (crs != NONE32) a_cr.issue(&d.acc[crs].credits_posted, a, small);
+      if (chg.mark) {  // write-back stream (changes.h): the owned accounts this window changed
+        if (drs != NONE32) chg.mark[drs] = chg_epoch;
+        if (crs != NONE32) chg.mark[crs] = chg_epoch;
+      }
       if (ins) {
         const uint64_t slot = xbase + rins;
         tb_transfer_t t2 = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];

@@ -332,3 +332,75 @@ extern "C" int tbg_gen_transfers_cfg4(void* d_out, uint64_t first, uint64_t coun
                                                                    n_accounts, batch, id_offset);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Id orders of the reference benchmark (`tigerbeetle benchmark --id-order`, cli.zig:97, 263-265;
+// benchmark_load.zig:122-126, 222, 292-300): every account id and transfer id is
+// IdPermutation.encode(index + 1) (testing/id.zig:8-48):
+//   sequential  identity:  data
+//   reversed    inversion: maxInt(u128) - data
+//   random      pseudo-UUID: data << 32 | (Xoshiro256(seed +% data).int(u128) & ~(maxInt(u64) << 32))
+// Zig std's DefaultPrng is Xoshiro256++ seeded through SplitMix64, and Random.int(u128) reads two
+// next() words little-endian, so the ids are the reference's own for the same permutation seed
+// (benchmark_load.zig:120-125 draws it as the first u64 of DefaultPrng.init(seed)).
+// k_permute_ids rewrites, in place, the ids of records generated with sequential ids (data = the
+// stored low word): an account's id; a transfer's id, debit and credit account ids and pending_id
+// (one bijection for all, so a stream keeps its outcomes under any order).
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline uint64_t wl_rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+__host__ __device__ inline tb_uint128_t wl_encode_id(uint64_t data, uint32_t order, uint64_t seed) {
+  tb_uint128_t id;
+  if (order == 1) {
+    uint64_t s[4], z = seed + data;  // DefaultPrng.init(seed +% data): SplitMix64 seeding
+    for (int k = 0; k < 4; k++) {
+      z += 0x9e3779b97f4a7c15ull;
+      uint64_t x = z;
+      x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+      x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+      s[k] = x ^ (x >> 31);
+    }
+    uint64_t r[2];
+    for (int k = 0; k < 2; k++) {  // xoshiro256++ next()
+      r[k] = wl_rotl(s[0] + s[3], 23) + s[0];
+      const uint64_t t = s[1] << 17;
+      s[2] ^= s[0];
+      s[3] ^= s[1];
+      s[1] ^= s[2];
+      s[0] ^= s[3];
+      s[2] ^= t;
+      s[3] = wl_rotl(s[3], 45);
+    }
+    id.lo = (data << 32) | (r[0] & 0xFFFFFFFFull);
+    id.hi = (data >> 32) | (r[1] & 0xFFFFFFFF00000000ull);
+  } else if (order == 2) {
+    id.lo = ~data;
+    id.hi = ~0ull;
+  } else {
+    id.lo = data;
+    id.hi = 0;
+  }
+  return id;
+}
+
+__global__ void k_permute_ids(uint8_t* recs, uint64_t count, uint32_t transfers, uint32_t order, uint64_t seed) {
+  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  tb_uint128_t* r = reinterpret_cast<tb_uint128_t*>(recs + k * 128);
+  // id (0); transfers: debit_account_id (1), credit_account_id (2), pending_id (4)
+  const int fields[4] = {0, 1, 2, 4};
+  const int n = transfers ? 4 : 1;
+  for (int j = 0; j < n; j++) {
+    tb_uint128_t& v = r[fields[j]];
+    if (v.hi == 0 && v.lo != 0) v = wl_encode_id(v.lo, order, seed);  // 0 and ids >= 2^64 stay
+  }
+}
+
+extern "C" int tbg_gen_permute_ids(void* d_records, uint64_t count, uint32_t transfers, uint32_t order, uint64_t seed,
+                                   void* stream) {
+  if (order > 2) return -1;
+  if (!count || order == 0) return 0;
+  k_permute_ids<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>((uint8_t*)d_records, count,
+                                                                                transfers, order, seed);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

@@ -87,12 +87,12 @@ class ShardedStateMachine:
     across all shards (None for a single shard)."""
 
     def __init__(self, shard_count, shard_index, exchange=None, device=0, batch_max=8190, accounts_max=1 << 16,
-                 transfers_max=1 << 20, window_events_max=0):
+                 transfers_max=1 << 20, window_events_max=0, change_log=False):
         import torch
 
         self.sm = StateMachine(device=device, batch_max=batch_max, accounts_max=accounts_max,
                                transfers_max=transfers_max, window_events_max=window_events_max,
-                               shard_count=shard_count, shard_index=shard_index)
+                               shard_count=shard_count, shard_index=shard_index, change_log=change_log)
         self.shard_count, self.shard_index = shard_count, shard_index
         self.batch_max, self.device = batch_max, device
         self.scratch = None
@@ -172,6 +172,61 @@ class ShardedStateMachine:
     # General class (csrc/shard_gx.inc): one batch at a time, decided on every shard from the
     # gathered read set by a scratch unsharded engine.
     # --------------------------------------------------------------------------------------------
+    # --------------------------------------------------------------------------------------------
+    # The rest of the StateMachine surface on a shard (csrc/shard_read.inc, tbg_open, the write-back
+    # stream): every shard gets the same call; reads gather from the owners through the exchange.
+    # --------------------------------------------------------------------------------------------
+    def open(self, accounts, transfers, pending_status, account_balances=None):
+        """StateMachine.open (state_machine.zig:527-541): the same whole set of forest objects on every
+        shard; each keeps what it owns."""
+        self.sm.open(accounts, transfers, pending_status, account_balances)
+        self._pulse_next = None
+
+    def read_request(self, operation, data):
+        """Step 1 of a lookup or query: this shard's part of the read buffer (to be summed)."""
+        import torch
+
+        L = _lib.lib()
+        op = int(operation)
+        dev = torch.device("cuda", self.device)
+        if op in (int(Operation.lookup_accounts), int(Operation.lookup_transfers)):
+            buf = torch.zeros(max(int(L.tbg_shard_lookup_bytes(len(data) // 16)), 1), dtype=torch.uint8, device=dev)
+            raw = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+            _lib.check(L.tbg_shard_lookup(self.sm.h, op, raw.ctypes.data, len(data), buf.data_ptr()), "shard_lookup")
+        else:
+            buf = torch.zeros(int(L.tbg_shard_query_bytes(self.shard_count, self.batch_max)), dtype=torch.uint8,
+                              device=dev)
+            raw = np.frombuffer(data, np.uint8)
+            _lib.check(L.tbg_shard_query(self.sm.h, op, raw.ctypes.data, len(data), buf.data_ptr()), "shard_query")
+        self.stream.synchronize()
+        return buf
+
+    def read_reply(self, operation, data, buf):
+        """Step 2 (after the buffers were summed): the reply bytes."""
+        L = _lib.lib()
+        op = int(operation)
+        out = self.sm._out
+        n = ctypes.c_uint64()
+        if op in (int(Operation.lookup_accounts), int(Operation.lookup_transfers)):
+            _lib.check(L.tbg_shard_lookup_reply(self.sm.h, buf.data_ptr(), len(data), out.ctypes.data, len(out),
+                                                ctypes.byref(n)), "shard_lookup_reply")
+        else:
+            raw = np.frombuffer(data, np.uint8)
+            _lib.check(L.tbg_shard_query_merge(self.sm.h, op, raw.ctypes.data, buf.data_ptr(), out.ctypes.data,
+                                               len(out), ctypes.byref(n)), "shard_query_merge")
+        return out[: n.value].tobytes()
+
+    def read(self, operation, data):
+        """lookup_* / get_account_* with this process's exchange: the reply bytes."""
+        buf = self.read_request(operation, data)
+        if self.exchange is not None:
+            self.exchange(buf)
+        return self.read_reply(operation, data, buf)
+
+    def window_changes(self):
+        """The write-back stream of this shard's last commit (its own objects)."""
+        return self.sm.window_changes()
+
     def pulse_next(self):
         """pulse_next_timestamp, the same on every shard. Cached: an order-free window holds no
         pending transfer and no timeout, so only the general path and pulses change it."""
@@ -273,7 +328,9 @@ class ShardedStateMachine:
                                    ctypes.c_uint64(), ctypes.c_uint64())
         _lib.check(L.tbg_device_state(sc.h, ctypes.byref(pa), ctypes.byref(na), ctypes.byref(px), ctypes.byref(ps),
                                       ctypes.byref(nx), ctypes.byref(pn2)), "device_state")
-        _lib.check(L.tbg_shard_apply(self.sm.h, pa, na.value, px, ps, nx.value, pn2.value), "shard_apply")
+        ph, phs = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(L.tbg_device_history(sc.h, ctypes.byref(ph), ctypes.byref(phs)), "device_history")
+        _lib.check(L.tbg_shard_apply(self.sm.h, pa, na.value, px, ps, nx.value, ph, phs, pn2.value), "shard_apply")
         self.sm.sync()
         self._pulse_next = pn2.value
         return reply
@@ -332,6 +389,16 @@ def pulse_general(shards, summed, timestamp):
     summed([s.gather(op, 0, 0, timestamp, 2) for s in shards])
     for s in shards:
         s.decide_apply(Operation.pulse, 0, 0, timestamp)
+
+
+def read_general(shards, summed, operation, data):
+    """A lookup or query on `shards` (all shards in-process, or this process's one): each writes what
+    it owns, the buffers are summed, every shard builds the same reply."""
+    bufs = [s.read_request(operation, data) for s in shards]
+    summed(bufs)
+    replies = [s.read_reply(operation, data, b) for s, b in zip(shards, bufs)]
+    assert all(r == replies[0] for r in replies)
+    return replies[0]
 
 
 def commit_general_batch(shards, summed, operation, d_events, n, timestamp, auto_pulse=True):

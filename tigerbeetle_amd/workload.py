@@ -198,3 +198,82 @@ def transfers_cfg4(first, count, seed, n_accounts, batch, id_offset=0):
     t["credit_account_id_lo"] = np.where(inj_cr, t["debit_account_id_lo"], t["credit_account_id_lo"])
     t["flags"] = flags
     return t
+
+
+# ------------------------------------------------------------------------------------------------
+# Id orders of `tigerbeetle benchmark --id-order` (csrc/workload.hip k_permute_ids): the reference's
+# IdPermutation.encode (testing/id.zig:8-48) with Zig std's DefaultPrng (Xoshiro256++, SplitMix64
+# seeding).
+# ------------------------------------------------------------------------------------------------
+ID_ORDERS = {"sequential": 0, "random": 1, "reversed": 2}
+_M64 = (1 << 64) - 1
+
+
+def _splitmix_seed(z):
+    """The four Xoshiro256 state words of DefaultPrng.init(z) (uint64 arrays)."""
+    out = []
+    with np.errstate(over="ignore"):
+        for _ in range(4):
+            z = z + np.uint64(0x9E3779B97F4A7C15)
+            x = z
+            x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            out.append(x ^ (x >> np.uint64(31)))
+    return out
+
+
+def _rotl(x, k):
+    return (x << np.uint64(k)) | (x >> np.uint64(64 - k))
+
+
+def _xoshiro_next(s):
+    with np.errstate(over="ignore"):
+        r = _rotl(s[0] + s[3], 23) + s[0]
+        t = s[1] << np.uint64(17)
+        s[2] ^= s[0]
+        s[3] ^= s[1]
+        s[1] ^= s[2]
+        s[0] ^= s[3]
+        s[2] ^= t
+        s[3] = _rotl(s[3], 45)
+    return r
+
+
+def benchmark_permutation_seed(seed):
+    """The random IdPermutation's seed the reference benchmark draws: DefaultPrng.init(seed), first
+    random.int(u64) (benchmark_load.zig:120-125)."""
+    s = _splitmix_seed(np.array([seed], np.uint64))
+    return int(_xoshiro_next(s)[0])
+
+
+def encode_ids(data, order, seed=0):
+    """IdPermutation.encode(data) for uint64 `data` (> 0): (lo, hi) uint64 arrays."""
+    data = np.asarray(data, np.uint64)
+    if order == 0:
+        return data.copy(), np.zeros_like(data)
+    if order == 2:
+        return ~data, np.full_like(data, np.uint64(_M64))
+    with np.errstate(over="ignore"):
+        s = _splitmix_seed(data + np.uint64(seed))
+    r0 = _xoshiro_next(s)
+    r1 = _xoshiro_next(s)
+    lo = (data << np.uint64(32)) | (r0 & np.uint64(0xFFFFFFFF))
+    hi = (data >> np.uint64(32)) | (r1 & np.uint64(0xFFFFFFFF00000000))
+    return lo, hi
+
+
+def permute_ids(recs, order, seed=0):
+    """Numpy twin of tbg_gen_permute_ids: records generated with sequential ids, rewritten in place
+    (accounts: id; transfers: id, debit and credit account ids, pending_id; 0 and ids >= 2^64
+    stay)."""
+    if order == 0:
+        return recs
+    fields = ["id"] + (["debit_account_id", "credit_account_id", "pending_id"]
+                       if "debit_account_id_lo" in recs.dtype.names else [])
+    for f in fields:
+        lo, hi = recs[f + "_lo"], recs[f + "_hi"]
+        m = (hi == 0) & (lo != 0)
+        elo, ehi = encode_ids(lo, order, seed)
+        recs[f + "_lo"] = np.where(m, elo, lo)
+        recs[f + "_hi"] = np.where(m, ehi, hi)
+    return recs
