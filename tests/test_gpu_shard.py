@@ -335,7 +335,7 @@ def test_shard_rejects_windows_outside_class(kind):
         a = workload.accounts(0, n_acc + 1, seed=3)
         a["flags"][5] = 2  # account 6: debits_must_not_exceed_credits
         a["flags"][n_acc] = 8  # account 65 (outside the uniform stream): flags.history
-        sh.commit_window(Operation.create_accounts, [a])
+        sh.commit_window(Operation.create_accounts, [a[:n_acc], a[n_acc:]])  # batch_max 64
         t = workload.transfers_uniform(0, 40, seed=3, n_accounts=n_acc)
         t["debit_account_id_lo"] = np.where(t["debit_account_id_lo"] == 6, 7, t["debit_account_id_lo"])
         t["credit_account_id_lo"] = np.where(t["credit_account_id_lo"] == 7, 8, t["credit_account_id_lo"])
