@@ -46,7 +46,7 @@ sys.path.insert(0, ROOT)
 
 BATCH = 8190
 WINDOW_BATCHES_MAX = 128  # csrc/window.h MAXB: batches per commit window
-PHASES = ["prep", "resolve", "classify", "wcount", "wlist", "walk", "final", "pulse", "cpw"]
+PHASES = ["prep", "resolve", "classify", "wcount", "wlist", "walk", "final", "pulse", "cpw", "fused"]
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
 NS_PER_S = 1_000_000_000
 
@@ -61,6 +61,8 @@ PHASE_ALG_BYTES = {
     "final": 2 * 128 + 2 * 32 + 16,
     # the chunked resolver (balance-limit windows): per event side its amount 16 and its check bit
     "resolve": 2 * (16 + 1),
+    # the fused pass (csrc/fused.h) moves the whole path in one launch: all of SURVEY 8(d)'s 640 B
+    "fused": 640,
 }
 # the kernels each timed phase launches (the first is the one named in `roofline.kernel`)
 PHASE_KERNELS = {
@@ -70,6 +72,7 @@ PHASE_KERNELS = {
     "cpw": ["k_cc_walk<true>", "k_cc_init", "k_cc_link", "k_cc_keys", "onesweep sort", "k_cc_segs"],
     "classify": ["k_classify<true>"], "wlist": ["k_wlist"], "walk": ["k_walk<true>", "k_wfold"],
     "pulse": ["k_pulse", "k_xwin_rb", "k_xwin_minlive", "k_xwin_replay", "k_xwin_expire"],
+    "fused": ["k_ct_fused", "k_fu_post"],
 }
 # the walkers (cpw, walk) run the reference loop for the events they decide: event 128, balance
 # pairs 2 x 32, record 128 per walked event

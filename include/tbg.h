@@ -52,6 +52,9 @@ typedef struct tbg_config {
 /* Resolve balance-limit windows with the grid-wide windowed relaxation (relax.h) even when their
    hot accounts fit the single-workgroup chunked resolver (chunks.h, the default). Same results. */
 #define TBG_FLAG_NO_CHUNKS 32u
+/* Commit every transfer window through the general path (no one-pass fused commit of order-free
+   windows, tigerbeetle_amd/csrc/fused.h). Same results; for A/B timing and tests. */
+#define TBG_FLAG_NO_FUSED 64u
 
 #define TBG_OK 0
 #define TBG_E_INVALID (-1)   /* input_valid() would reject the request */
@@ -334,6 +337,7 @@ typedef struct tbg_stats {
     uint64_t component_events; /* of which component-parallel walkers decided */
     uint64_t sorted_transfers; /* leading transfer records in the sorted id prefix (not hashed) */
     uint64_t chunked_windows;  /* balance-limit windows the chunked resolver decided */
+    uint64_t fused_windows;    /* order-free transfer windows committed in one pass (fused.h) */
 } tbg_stats;
 int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
 

@@ -1,0 +1,201 @@
+"""The fused pass (tigerbeetle_amd/csrc/fused.h): an order-free create_transfers window committed in
+one launch must give exactly what the general path and the CPU restatement give (per-batch replies,
+every stored record and status, lookups afterwards). Covered: windows with static failures and
+retries of stored ids (exists codes), monotonic windows whose records are hashed instead of
+extending the sorted prefix (k_fu_post indexing), and windows that leave the class partway (every
+block's speculative balance adds undone, then the general path), each kind followed by more simple
+windows so the back-off re-arms the speculation."""
+import numpy as np
+import pytest
+
+from oracle_sm import OracleStateMachine
+from test_gpu_parity import _compare_final
+from test_gpu_window import commit_window, oracle_batches
+from tigerbeetle_amd import workload
+from tigerbeetle_amd.types import Operation
+
+BM = 1024  # events per batch
+WIN = 8    # batches per window
+
+
+def _engines(n_acc, n_xfer, fused=True):
+    from tigerbeetle_amd import StateMachine
+
+    gpu = StateMachine(batch_max=BM, accounts_max=n_acc + 8, transfers_max=n_xfer, window_events_max=WIN * BM,
+                       fused=fused)
+    ref = OracleStateMachine(batch_max=BM)
+    return gpu, ref
+
+
+def _accounts(gpu, ref, n_acc, flags=None):
+    acc = workload.accounts(0, n_acc, seed=11)
+    if flags:
+        for slot, fl in flags.items():
+            acc["flags"][slot] = fl
+    batches = [acc[f:f + BM] for f in range(0, n_acc, BM)]
+    assert commit_window(gpu, Operation.create_accounts, batches) == oracle_batches(ref, Operation.create_accounts,
+                                                                                   batches)
+
+
+def _window(first, n_acc, seed=11, id_offset=0):
+    t = workload.transfers_uniform(first, WIN * BM, seed=seed, n_accounts=n_acc, id_offset=id_offset)
+    return [t[k * BM:(k + 1) * BM].copy() for k in range(WIN)]
+
+
+def _check(gpu, ref, batches):
+    g = commit_window(gpu, Operation.create_transfers, batches)
+    r = oracle_batches(ref, Operation.create_transfers, batches)
+    for b, (x, y) in enumerate(zip(g, r)):
+        assert x == y, (b, np.frombuffer(x, "<u4")[:16], np.frombuffer(y, "<u4")[:16])
+
+
+def _inject_static_failures(batches, rng, n_acc):
+    """Failures every decision of which is static (validation, lookups, ledgers): the window stays
+    in the fused class and its ranks shift."""
+    for ev in batches:
+        k = rng.choice(BM, size=24, replace=False)
+        ev["ledger"][k[0:4]] = 3                     # transfer_must_have_the_same_ledger_as_accounts
+        ev["debit_account_id_lo"][k[4:8]] = n_acc + 100   # debit_account_not_found
+        ev["credit_account_id_lo"][k[8:10]] = n_acc + 101  # credit_account_not_found
+        ev["amount_lo"][k[10:13]] = 0                 # amount_must_not_be_zero
+        ev["timestamp"][k[13:15]] = 7                 # timestamp_must_be_zero
+        ev["flags"][k[15:17]] = 1 << 9                # reserved_flag (padding bit)
+        ev["code"][k[17:19]] = 0                      # code_must_not_be_zero
+        ev["credit_account_id_lo"][k[19:21]] = ev["debit_account_id_lo"][k[19:21]]  # accounts_must_be_different
+        ev["timeout"][k[21:24]] = 5                   # timeout_reserved_for_pending_transfer
+
+
+@pytest.mark.gpu
+def test_fused_matches_oracle_with_static_failures_and_retries():
+    n_acc = 3000
+    gpu, ref = _engines(n_acc, 1 << 19)
+    rng = np.random.default_rng(5)
+    try:
+        _accounts(gpu, ref, n_acc)
+        first = 0
+        for w in range(6):
+            batches = _window(first, n_acc)
+            first += WIN * BM
+            if w % 2 == 1:
+                _inject_static_failures(batches, rng, n_acc)
+            _check(gpu, ref, batches)
+        assert gpu.stats()["fused_windows"] == 6
+        assert gpu.stats()["sorted_transfers"] == gpu.stats()["transfers"]
+        # retries: the stored ids again (exists / exists_with_different_*), still increasing, then new
+        # ids: first id below x_id_max, so the window's records are hashed (not the sorted prefix)
+        old = _window(WIN * BM, n_acc)  # window 1's ids (with some fields changed below)
+        flat = np.concatenate(old)
+        flat["amount_lo"][::7] += 1
+        flat["user_data_64"][::11] ^= 1
+        retry = np.concatenate([flat[:3 * BM], workload.transfers_uniform(first, 5 * BM, seed=12, n_accounts=n_acc)])
+        first += 5 * BM
+        batches = [retry[k * BM:(k + 1) * BM].copy() for k in range(WIN)]
+        _check(gpu, ref, batches)
+        st = gpu.stats()
+        assert st["fused_windows"] == 7
+        assert st["sorted_transfers"] < st["transfers"]  # the prefix froze: records hashed by k_fu_post
+        # later monotonic windows stay fused and hashed; a retry of hashed ids finds them
+        for w in range(2):
+            batches = _window(first, n_acc, seed=13)
+            first += WIN * BM
+            _check(gpu, ref, batches)
+        hashed = np.concatenate([retry[3 * BM:], np.concatenate(batches)])[:WIN * BM]
+        _check(gpu, ref, [hashed[k * BM:(k + 1) * BM].copy() for k in range(WIN)])
+        assert gpu.stats()["fused_windows"] == 10
+        ids = np.concatenate([retry["id_lo"][:50], hashed["id_lo"][-50:], np.array([first + 10**6], np.uint64)])
+        q = np.zeros(len(ids), [("lo", "<u8"), ("hi", "<u8")])
+        q["lo"] = ids
+        assert gpu.commit(0, 99, 0, Operation.lookup_transfers, q.tobytes()) == \
+            ref.commit(0, 99, 0, Operation.lookup_transfers, q.tobytes())
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+OUT_OF_CLASS = ["pending", "linked", "limit", "history", "order", "huge", "balancing", "post"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", OUT_OF_CLASS)
+@pytest.mark.parametrize("where", ["first", "last"])
+def test_fused_speculation_undone(kind, where):
+    """One event outside the class (first or last block of the window): the blocks that applied
+    their balance adds are undone, the general path commits the window, replies and stores equal the
+    restatement's; simple windows after it go back to the fused pass."""
+    n_acc = 2000
+    # two accounts the uniform stream never touches: n_acc + 1 debits_must_not_exceed_credits,
+    # n_acc + 2 flags.history
+    gpu, ref = _engines(n_acc, 1 << 19)
+    try:
+        _accounts(gpu, ref, n_acc + 2, flags={n_acc: 2, n_acc + 1: 8})
+        first = 0
+        for w in range(2):
+            _check(gpu, ref, _window(first, n_acc))
+            first += WIN * BM
+        batches = _window(first, n_acc)
+        first += WIN * BM
+        b, j = (0, 3) if where == "first" else (WIN - 1, BM - 5)
+        ev = batches[b]
+        if kind == "pending":
+            ev["flags"][j] = 2
+            ev["timeout"][j] = 30
+        elif kind == "linked":
+            ev["flags"][j] = 1
+        elif kind == "limit":
+            ev["debit_account_id_lo"][j] = n_acc + 1
+            ev["credit_account_id_lo"][j] = 9
+        elif kind == "history":
+            ev["debit_account_id_lo"][j] = 9
+            ev["credit_account_id_lo"][j] = n_acc + 2
+        elif kind == "order":  # an id below its predecessor's: not claim-free
+            ev["id_lo"][j] = ev["id_lo"][j - 2]
+        elif kind == "huge":
+            ev["amount_lo"][j] = 1 << 50
+        elif kind == "balancing":
+            ev["flags"][j] = 16
+        elif kind == "post":
+            ev["flags"][j] = 4
+            ev["pending_id_lo"][j] = 17
+            ev["amount_lo"][j] = 0
+        _check(gpu, ref, batches)
+        assert gpu.stats()["fused_windows"] == 2
+        for w in range(6):  # back-off: two general-path windows, then fused again
+            _check(gpu, ref, _window(first, n_acc))
+            first += WIN * BM
+        assert gpu.stats()["fused_windows"] >= 5
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_fused_equals_general_path_digest():
+    """The same uniform stream through the fused pass and through the general path (fused off):
+    identical digests and dumps."""
+    n_acc = 4000
+    a, ref = _engines(n_acc, 1 << 19, fused=True)
+    b, _ = _engines(n_acc, 1 << 19, fused=False)
+    rng = np.random.default_rng(9)
+    try:
+        _accounts(a, ref, n_acc)
+        acc = workload.accounts(0, n_acc, seed=11)
+        commit_window(b, Operation.create_accounts, [acc[f:f + BM] for f in range(0, n_acc, BM)])
+        first = 0
+        for w in range(5):
+            batches = _window(first, n_acc, seed=21)
+            first += WIN * BM
+            if w == 2:
+                _inject_static_failures(batches, rng, n_acc)
+            ga = commit_window(a, Operation.create_transfers, batches)
+            gb = commit_window(b, Operation.create_transfers, batches)
+            assert ga == gb
+        assert a.stats()["fused_windows"] == 5 and b.stats()["fused_windows"] == 0
+        assert a.digest() == b.digest()
+        assert a.dump_accounts().tobytes() == b.dump_accounts().tobytes()
+        assert a.dump_transfers().tobytes() == b.dump_transfers().tobytes()
+    finally:
+        a.close()
+        b.close()
+        ref.close()

@@ -47,6 +47,7 @@ FLAG_RES_WAIT = 4
 FLAG_CHANGE_LOG = 8
 FLAG_NO_XWIN = 16
 FLAG_NO_CHUNKS = 32
+FLAG_NO_FUSED = 64
 
 
 class Stats(ctypes.Structure):
@@ -54,7 +55,8 @@ class Stats(ctypes.Structure):
                 ("expiry_entries", ctypes.c_uint64), ("pulse_next_timestamp", ctypes.c_uint64),
                 ("events_total", ctypes.c_uint64), ("walker_events", ctypes.c_uint64),
                 ("resolver_events", ctypes.c_uint64), ("component_events", ctypes.c_uint64),
-                ("sorted_transfers", ctypes.c_uint64), ("chunked_windows", ctypes.c_uint64)]
+                ("sorted_transfers", ctypes.c_uint64), ("chunked_windows", ctypes.c_uint64),
+                ("fused_windows", ctypes.c_uint64)]
 
 
 class Demuxer(ctypes.Structure):

@@ -19,7 +19,7 @@
 
 __device__ inline bool cpw_active(const Globals* g) {
   // windows with history rows need the exact balances after each event: sequential walker
-  return !WIN_REJECTED(g) && !g->hot_count && !window_ovf_mode(g) && !(g->win_flags & 16u);
+  return !WIN_REJECTED(g) && !SP_DONE(g) && !g->hot_count && !window_ovf_mode(g) && !(g->win_flags & 16u);
 }
 
 __device__ inline uint32_t cc_find(const uint32_t* parent, uint32_t x) {

@@ -131,7 +131,21 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t res_chunk_windows;  // cumulative windows the chunked resolver decided
   uint32_t cpw_want;  // last window: W events in a window the component walkers could take (host readback)
   uint32_t rc_last;   // last window: the chunked resolver decided it (host readback, read with cpw_want)
+  // fused pass (fused.h): sp_done = the fused pass committed the current window (the general path's
+  // kernels return at once); sp_state tells k_fu_post what is left (undo / index ids); sp_skip =
+  // transfer windows left before the next speculation (exponential back-off after sp_fails misses);
+  // fu_abort = epoch of the window a block found outside the class (later blocks skip their work)
+  uint32_t sp_done;
+  uint32_t sp_state;
+  uint32_t sp_skip;
+  uint32_t sp_fails;
+  uint32_t fu_abort;
+  uint32_t pad5;
+  uint64_t fu_windows;  // cumulative windows committed by the fused pass
 };
+
+// The fused pass (fused.h) committed this window: the general path's kernels return at once.
+#define SP_DONE(g) ((g)->sp_done != 0)
 
 // Whether this block is the last of its grid to arrive (every thread of every block calls it once).
 // Every thread's earlier writes are released device-wide first, so the last block, after its

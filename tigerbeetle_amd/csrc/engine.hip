@@ -160,7 +160,7 @@ __device__ inline void bind_add(Dev d, Scratch s, uint32_t* tk, unsigned long lo
 __global__ void __launch_bounds__(BIND_T) k_bind_sum(Dev d, Scratch s, uint32_t E, uint32_t epoch) {
   __shared__ uint32_t tk[BIND_LDS];
   __shared__ unsigned long long tv[BIND_LDS];
-  if (WIN_REJECTED(d.g) || !d.g->hot_count) return;
+  if (WIN_REJECTED(d.g) || SP_DONE(d.g) || !d.g->hot_count) return;
   for (uint32_t j = threadIdx.x; j < BIND_LDS; j += blockDim.x) {
     tk[j] = NONE32;
     tv[j] = 0;
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(BIND_T) k_bind_sum(Dev d, Scratch s, uint32_t 
 // Per hot rank: un-mark the account when its checks cannot fail this window.
 __global__ void __launch_bounds__(256) k_bind_decide(Dev d, Scratch s) {
   Globals* g = d.g;
-  if (WIN_REJECTED(g)) return;
+  if (WIN_REJECTED(g) || SP_DONE(g)) return;
   const uint32_t n = g->hot_count;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   bool cold = false;
@@ -217,7 +217,7 @@ __global__ void __launch_bounds__(256) k_bind_decide(Dev d, Scratch s) {
 
 // Every hot account non-binding: the window reads no balance after all (cpw / order-free paths).
 __global__ void k_bind_finish(Globals* g) {
-  if (WIN_REJECTED(g)) return;
+  if (WIN_REJECTED(g) || SP_DONE(g)) return;
   if (g->hot_count && g->cold_count == g->hot_count) g->hot_count = 0;
   g->cold_count = 0;
 }
@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   __shared__ unsigned long long id_max;  // largest id key this block may insert (Globals::x_id_max)
   __shared__ uint32_t marked[MARK_LDS];  // mark_first: accounts this block marks
   __shared__ uint32_t nfirst, fbase;      // accounts this block marked first, their first rank
-  if (WIN_REJECTED(d.g)) return;
+  if (WIN_REJECTED(d.g) || SP_DONE(d.g)) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   for (uint32_t j = threadIdx.x; j < MARK_LDS; j += blockDim.x) marked[j] = NONE32;
   if (threadIdx.x == 0) {
@@ -499,7 +499,7 @@ __device__ inline u128 block_sum_u128(u128 v, u128* lds) {
 __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t nblk) {
   __shared__ u128 red[1024];
   __shared__ uint32_t aux;
-  if (WIN_REJECTED(d.g)) return;
+  if (WIN_REJECTED(d.g) || SP_DONE(d.g)) return;
   if (threadIdx.x == 0) aux = 0;
   __syncthreads();
   u128 v = 0;
@@ -534,7 +534,7 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
 // that is not gets its key-map claims here, before anything reads the map.
 __global__ void __launch_bounds__(256) k_claim_fix(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, uint32_t E,
                                                    uint32_t epoch) {
-  if (WIN_REJECTED(d.g) || !d.g->mono_prev || (d.g->win_flags & 1u)) return;
+  if (WIN_REJECTED(d.g) || SP_DONE(d.g) || !d.g->mono_prev || (d.g->win_flags & 1u)) return;
   // grid-stride over a capped grid: the common case (speculation right) is a launch whose blocks
   // exit at once, so it pays for few blocks
   const uint8_t* evb = reinterpret_cast<const uint8_t*>(ev);
@@ -737,7 +737,7 @@ __device__ inline bool classify_event(const Dev& d, const Scratch& s, const WinD
 template <bool XFER>
 __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, uint32_t epoch) {
   __shared__ uint32_t lds[4];
-  if (WIN_REJECTED(d.g)) return;
+  if (WIN_REJECTED(d.g) || SP_DONE(d.g)) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   SegTally t{blockIdx.x * 256u / SEG, 0u};
   const bool ovf_mode = XFER && window_ovf_mode(d.g);
@@ -769,9 +769,9 @@ __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, u
 // ------------------------------------------------------------------------------------------------
 // The ordered W list (one event per thread, one 1024-event segment per block; k_classify counted).
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(SEG) k_wlist(Scratch s, uint32_t E) {
+__global__ void __launch_bounds__(SEG) k_wlist(const Globals* g, Scratch s, uint32_t E) {
   __shared__ uint32_t lds[SEG / 64];
-  if (s.cnt_w[blockIdx.x] == 0) return;  // uniform per block
+  if (SP_DONE(g) || s.cnt_w[blockIdx.x] == 0) return;  // uniform per block
   const uint32_t prefix = seg_prefix<SEG>(s.cnt_w, blockIdx.x, lds);
   const uint32_t i = blockIdx.x * SEG + threadIdx.x;
   const uint32_t w = (i < E && (s.cls[i] & C_W)) ? 1u : 0u;
@@ -791,7 +791,7 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
                                                         uint32_t nseg, uint32_t epoch) {
   __shared__ uint32_t lds[WALK_THREADS / 64];
   __shared__ uint32_t sbad[MAX_SEGS], sins[MAX_SEGS];
-  if (WIN_REJECTED(d.g)) return;
+  if (WIN_REJECTED(d.g) || SP_DONE(d.g)) return;
   if (threadIdx.x == 0) {
     Globals* g = d.g;
     g->base = XFER ? g->x_count : g->acc_count;
@@ -1164,7 +1164,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   __shared__ uint32_t lds[SEG / 64];
   __shared__ unsigned long long ldsm[SEG / 64];
   __shared__ uint4 stage[SEG * 8];  // one 128 B record per event: 128 KiB
-  if (WIN_REJECTED(d.g)) return;
+  if (WIN_REJECTED(d.g) || SP_DONE(d.g)) return;
   const bool prefix_win = XFER && (d.g->win_flags & 2u) != 0;  // k_prep_reduce
   const uint32_t E = w.E;
   const uint32_t i = blockIdx.x * SEG + threadIdx.x;
@@ -1385,6 +1385,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
       gw->ovf_bound = (gw->batch_huge || sum < gw->ovf_bound) ? MAX128 : sum;
       gw->batch_amount_sum = 0;
       gw->batch_huge = 0;
+      if (gw->sp_skip) gw->sp_skip--;  // the fused pass's back-off (fused.h)
     } else {
       gw->acc_count = xbase + total_ins;
     }
@@ -1416,6 +1417,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   }
 }
 
+#include "fused.h"
 #include "shard.h"
 
 // ------------------------------------------------------------------------------------------------

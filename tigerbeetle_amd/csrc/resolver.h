@@ -98,6 +98,7 @@ __global__ void __launch_bounds__(256) k_res_keys(Dev d, Scratch s, uint32_t E, 
                                                   uint32_t allow_relax) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   Globals* g = d.g;
+  if (SP_DONE(g)) return;
   bool active = !g->res_inelig && g->hot_count;
   if (active && i < g->hot_count) {
     s.rstate[i].start = 0;

@@ -30,14 +30,16 @@ def to_host(t):
 class StateMachine:
     def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20,
                  window_events_max=0, resolver=True, components=True, shard_count=0, shard_index=0,
-                 change_log=False):
+                 change_log=False, fused=True):
         L = _lib.lib()
         # resolver: True = chunked single-workgroup resolver (chunks.h) where the window fits it, else
         # windowed relaxation (relax.h); "relax" = relaxation only; "wait" = wait-based walkers
         # (resolver.h); False = sequential walker only
         flags = ((0 if resolver else _lib.FLAG_NO_RESOLVER) | (0 if components else _lib.FLAG_NO_COMPONENTS) |
                  (_lib.FLAG_RES_WAIT if resolver == "wait" else 0) |
-                 (_lib.FLAG_NO_CHUNKS if resolver == "relax" else 0) | (_lib.FLAG_CHANGE_LOG if change_log else 0))
+                 (_lib.FLAG_NO_CHUNKS if resolver == "relax" else 0) | (_lib.FLAG_CHANGE_LOG if change_log else 0) |
+                 (0 if fused else _lib.FLAG_NO_FUSED))
+        # fused: order-free transfer windows may commit in one pass (csrc/fused.h); False = general path
         cfg = _lib.Config(device, batch_max, accounts_max, transfers_max, window_events_max, flags, shard_count,
                           shard_index)
         h = ctypes.c_void_p()
