@@ -132,15 +132,17 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t cpw_want;  // last window: W events in a window the component walkers could take (host readback)
   uint32_t rc_last;   // last window: the chunked resolver decided it (host readback, read with cpw_want)
   // fused pass (fused.h): sp_done = the fused pass committed the current window (the general path's
-  // kernels return at once); sp_state tells k_fu_post what is left (undo / index ids); sp_skip =
+  // kernels return at once); sp_skip =
   // transfer windows left before the next speculation (exponential back-off after sp_fails misses);
   // fu_abort = epoch of the window a block found outside the class (later blocks skip their work)
   uint32_t sp_done;
-  uint32_t sp_state;
   uint32_t sp_skip;
   uint32_t sp_fails;
   uint32_t fu_abort;
-  uint32_t pad5;
+  uint32_t fu_epoch;    // the window k_ct_fused ran for (not backed off)
+  uint32_t fu_prefix;   // that window extends the sorted prefix (captured before k_fu_final updates it)
+  uint64_t fu_base;     // that window's first record slot
+  uint64_t fu_bad;      // that window's failures: [63:32] epoch | [31:0] count
   uint64_t fu_windows;  // cumulative windows committed by the fused pass
 };
 

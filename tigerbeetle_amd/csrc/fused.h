@@ -5,9 +5,11 @@
 // ~72 B of scratch columns per event and reads ~40 B of them back, in seven launches. For a window in
 // which every outcome is order-free that traffic buys nothing: k_ct_fused decides each event
 // (state_machine.zig:1462-1507 validation, lookups, ledgers, create_transfer_exists :1587-1606; the
-// balance tail :1509-1547 cannot fail, below), applies its balance effects (:1549-1575) and writes its
-// reply and record, in one launch. Ranks (reply slot, record slot) come from a decoupled look-back
-// over per-block status words instead of scratch columns.
+// balance tail :1509-1547 cannot fail, below), applies its balance effects (:1549-1575) and stores its
+// record in place (slot base + i, final when no earlier event of the window failed); k_fu_final then
+// writes the replies and moves the records after the window's first failure down to their ranks
+// (nothing to move in a window without failures). No block waits for another: a decoupled look-back
+// for the ranks measured 50 us per 1M-event window of blocks idling behind slower predecessors.
 //
 // Simple = every event of the window is either decided statically (validation, lookups, ledgers,
 // exists) or is a plain create (no linked / pending / post / void / balancing flag) whose accounts
@@ -18,37 +20,22 @@
 // Then every outcome is a function of the pre-window state and the event alone.
 //
 // Speculation. Each block applies its balance adds as soon as its own events are simple; whether the
-// whole window is simple is known only to the window's last block (its inclusive look-back). If it is
-// not, k_fu_post subtracts the adds of every block that applied (recomputing the same decisions from
-// the same unchanged inputs: nothing the decisions read is written here), and the general path runs
-// the window as if this kernel had not (its record, reply and status stores are all rewritten or
-// beyond the store's end). Globals::sp_done tells the general path's kernels to return at once when the
-// fused pass committed the window. A window that is not simple backs the speculation off
-// exponentially (Globals::sp_skip windows, k_final counts them down).
+// whole window is simple is known after the launch (Globals::fu_abort = this window's epoch when a
+// block was not). If it is not, k_fu_final subtracts the adds of every block that applied (recomputing
+// the same decisions from the same unchanged inputs: nothing the decisions read is written here), and
+// the general path runs the window as if this pass had not (its record and status stores are all
+// rewritten or beyond the store's end). Globals::sp_done tells the general path's kernels to return
+// at once when the fused pass committed the window. A window that is not simple backs the speculation
+// off exponentially (Globals::sp_skip windows, k_final counts them down).
 #pragma once
 
 #define FU_T 256
 #define FU_AMOUNT_MAX (1ull << 43)  // per-event amount bound: 2^20 events x 2^43 <= 2^63
-// Globals::sp_state after a fused launch (read by k_fu_post)
-enum : uint32_t { FU_STATE_NONE = 0, FU_STATE_UNDO = 1, FU_STATE_INSERT = 2 };
-// look-back status word per block: [63:32] window epoch | [31:30] state | [29] not simple | [20:0] failures
-enum : uint32_t { FU_AGG = 1u, FU_INC = 2u };
-#define FU_SPIN_MAX (1u << 22)  // bounded look-back wait (a stuck predecessor fails the speculation)
+// timing experiments only (results wrong): 1 no balance adds, 4 no record stores
+#ifndef FU_EXP
+#define FU_EXP 0
+#endif
 
-__device__ __forceinline__ unsigned long long fu_word(uint32_t epoch, uint32_t state, bool not_simple, uint32_t bad) {
-  return ((unsigned long long)epoch << 32) | ((unsigned long long)state << 30) | (not_simple ? (1ull << 29) : 0ull) |
-         (unsigned long long)(bad & 0x1FFFFFu);
-}
-__device__ __forceinline__ uint32_t fu_state(unsigned long long w) { return (uint32_t)(w >> 30) & 3u; }
-__device__ __forceinline__ bool fu_not_simple(unsigned long long w) { return (w >> 29) & 1ull; }
-__device__ __forceinline__ uint32_t fu_bad(unsigned long long w) { return (uint32_t)w & 0x1FFFFFu; }
-
-__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -134,36 +121,64 @@ __device__ __forceinline__ void fu_decide(const Dev& d, const tb_transfer_t* __r
 
 // Scratch of the fused pass (per 256-event block; per 64-event wave).
 struct FuScratch {
-  unsigned long long* st;   // look-back status words
-  unsigned long long* pay;  // per block: [4k] aggregate sum, [4k+1] aggregate id max, [4k+2..3] inclusive
-  uint8_t* applied;         // per block: its balance adds were applied (k_fu_post undoes them)
-  unsigned long long* ok;   // per wave: ok-event bitmap (k_fu_post indexes a non-prefix window's ids)
+  uint32_t* cnt;            // per block: failed events
+  unsigned long long* pay;  // per block: [2k] its reaching amounts' sum, [2k+1] its largest reaching id
+  uint8_t* applied;         // per block: its balance adds were applied (k_fu_final undoes them)
+  unsigned long long* ok;   // per wave: ok-event bitmap
 };
 
-__global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, FuScratch fs, const tb_transfer_t* __restrict__ ev,
-                                                   WinDesc w, uint32_t epoch, FinalOut o) {
-  __shared__ uint4 stage[FU_T * 4];     // half of each inserted record per round (16 KiB)
+__device__ __forceinline__ void fu_store_records(Dev d, const tb_transfer_t& t, bool ok, unsigned long long okm,
+                                                 uint64_t first_slot, uint4* ws) {
+  // the wave's ok records as one contiguous run from first_slot, through LDS in two halves of 64 B
+  // (each store instruction writes whole 64 B sectors)
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nins = (uint32_t)__popcll(okm);
+  const uint32_t pos = ok ? (uint32_t)__popcll(okm & ((1ull << lane) - 1ull)) : 0u;
+  const uint4* src = reinterpret_cast<const uint4*>(&t);
+  uint4* dst = reinterpret_cast<uint4*>(d.xr + first_slot);
+#pragma unroll
+  for (int half = 0; half < 2; half++) {
+    wave_sync();
+    if (ok) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) ws[pos * 4 + q] = src[half * 4 + q];
+    }
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t idx = c * 64 + lane, r = idx >> 2, q = idx & 3;
+      if (r < nins) st_stream(dst + r * 8 + half * 4 + q, ws[idx]);
+    }
+  }
+}
+
+// Decide, apply, store in place. Writes nothing but scratch, the in-place records and statuses (slots
+// at or beyond the store's end) and, when its events are simple, the balance adds.
+__global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
+                                                   WinDesc w, uint32_t epoch) {
+  __shared__ uint4 stage[FU_T * 4];  // half of each inserted record per round (16 KiB)
   __shared__ uint32_t lds[FU_T / 64];
   __shared__ unsigned long long ldsu[2 * (FU_T / 64)];
-  __shared__ uint32_t sh_ex_bad, sh_ns;
   Globals* g = d.g;
   if (WIN_REJECTED(g)) return;
+  const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (g->sp_skip) {  // backed off: the general path decides this window
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      g->sp_done = 0;
-      g->sp_state = FU_STATE_NONE;
-    }
+    if (k == 0 && threadIdx.x == 0) g->sp_done = 0;
     return;
   }
-  const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t i = k * FU_T + threadIdx.x;
   const uint32_t E = w.E;
   const uint64_t base = g->x_count, x_id_max = g->x_id_max, P = g->x_sorted;
   const u128 ovf = g->ovf_bound;
-  // window-level conditions: the balance fields stay below 2^64 (ovf + 2^20 x 2^43 < 2^64)
+  // window-level condition: the balance fields stay below 2^64 (ovf + 2^20 x 2^43 < 2^64)
   const bool glob_ok = (uint64_t)(ovf >> 64) == 0 && (uint64_t)ovf < (1ull << 63) && !g->batch_huge;
-  // the window extends the sorted prefix (claim-free when simple; first id above every stored id)
-  const bool prefix_win = P == base && ev[0].id.hi == 0 && ev[0].id.lo > x_id_max;
+  if (k == 0 && threadIdx.x == 0) {
+    // what k_fu_final reads while its last block updates the store counts
+    g->fu_epoch = epoch;
+    g->fu_base = base;
+    // the window extends the sorted prefix (claim-free when simple; first id above every stored id)
+    g->fu_prefix = (P == base && ev[0].id.hi == 0 && ev[0].id.lo > x_id_max) ? 1u : 0u;
+  }
   const bool aborted = __hip_atomic_load(&g->fu_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
 
   tb_transfer_t t;
@@ -173,210 +188,91 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, FuScratch fs, const tb
   fe.code = TB_CT_OK;
   fe.amount = fe.id_key = 0;
   fe.dr = fe.cr = NONE32;
-  uint32_t b = 0;
   if (i < E && !aborted) {
     t = ev[i];
-    b = win_batch(w, i);
     fu_decide(d, ev, i, t, x_id_max, P, &fe);
-    t.timestamp = win_ts(w, b, i);  // :1253 (the record as inserted)
+    t.timestamp = win_ts(w, win_batch(w, i), i);  // :1253 (the record as inserted)
   }
   const bool blk_simple = __syncthreads_and(fe.simple) && glob_ok && !aborted;
+  if (threadIdx.x == 0) {
+    fs.applied[k] = blk_simple ? 1 : 0;
+    // (a later block that reads this skips its work; k_fu_final reads it after the launch)
+    if (!blk_simple && !aborted) __hip_atomic_store(&g->fu_abort, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!blk_simple) return;
   const bool ok = i < E && fe.code == TB_CT_OK;
-  if (blk_simple && ok) {
+  if (ok && !(FU_EXP & 1)) {
     // no-return 64-bit adds: every field stays below 2^64 this window (glob_ok, FU_AMOUNT_MAX)
     (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.dr].debits_posted), fe.amount);
     (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.cr].credits_posted), fe.amount);
   }
-  if (threadIdx.x == 0) {
-    fs.applied[k] = blk_simple ? 1 : 0;
-    if (!blk_simple && !aborted) __hip_atomic_store(&g->fu_abort, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  const bool bad = i < E && !ok;
+  if (bad) s.code[i] = fe.code;
   const unsigned long long okm = __ballot(ok);
   if (lane == 0 && i < E) fs.ok[i >> 6] = okm;
-
-  // this block's aggregate: failures, the reaching amounts' sum and the largest reaching id
-  const bool bad = i < E && !ok;
-  const uint32_t inc = wave_incl_scan(bad ? 1u : 0u);
+  if (ok) d.xstatus[base + i] = 0;
+  if (okm && !(FU_EXP & 4)) {  // in place: slot base + i
+    const uint32_t first = (uint32_t)__builtin_ctzll(okm);
+    fu_store_records(d, t, ok, okm, base + (i - lane) + first, stage + wave * 256);
+  }
+  // this block's failures, reaching amounts' sum and largest reaching id (k_fu_final folds them)
+  const uint32_t wbad = (uint32_t)__popcll(__ballot(bad));
   const unsigned long long wsum = wave_sum_u64(fe.reach ? fe.amount : 0ull);
   const unsigned long long wmax = wave_max_u64(fe.reach ? fe.id_key : 0ull);
-  if (lane == 63) lds[wave] = inc;
   if (lane == 0) {
+    lds[wave] = wbad;
     ldsu[2 * wave] = wsum;
     ldsu[2 * wave + 1] = wmax;
   }
   __syncthreads();
-  uint32_t wp = 0, nbad = 0;
-  unsigned long long bsum = 0, bmax = 0;
+  if (threadIdx.x == 0) {
+    uint32_t nbad = 0;
+    unsigned long long bsum = 0, bmax = 0;
 #pragma unroll
-  for (uint32_t q = 0; q < FU_T / 64; q++) {
-    if (q < wave) wp += lds[q];
-    nbad += lds[q];
-    bsum += ldsu[2 * q];
-    bmax = ldsu[2 * q + 1] > bmax ? ldsu[2 * q + 1] : bmax;
-  }
-
-  // Decoupled look-back (wave 0): publish the aggregate, then fold predecessors until an inclusive
-  // one. A block outside the class publishes "not simple" as its inclusive state at once (absorbing).
-  if (wave == 0) {
-    uint32_t ex_bad = 0;
-    unsigned long long ex_sum = 0, ex_max = 0;
-    bool ns = !blk_simple;
-    if (k > 0 && blk_simple) {
-      if (lane == 0) {
-        st_agent(&fs.pay[4 * k], bsum);
-        st_agent(&fs.pay[4 * k + 1], bmax);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // payload before the status word
-        st_agent(&fs.st[k], fu_word(epoch, FU_AGG, false, nbad));
-      }
-      int32_t pos = (int32_t)k - 1;
-      uint32_t spins = 0;
+    for (uint32_t q = 0; q < FU_T / 64; q++) {
+      nbad += lds[q];
+      bsum += ldsu[2 * q];
+      bmax = ldsu[2 * q + 1] > bmax ? ldsu[2 * q + 1] : bmax;
+    }
+    fs.cnt[k] = nbad;
+    fs.pay[2 * k] = bsum;
+    fs.pay[2 * k + 1] = bmax;
+    if (nbad) {
+      // the window's failure count, tagged with its epoch (no reset between windows)
+      unsigned long long* acc = reinterpret_cast<unsigned long long*>(&g->fu_bad);
+      unsigned long long old = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (;;) {
-        const int32_t j = pos - (int32_t)lane;
-        const unsigned long long wd = j >= 0 ? ld_agent(&fs.st[j]) : fu_word(epoch, FU_INC, false, 0);
-        const bool ready = (uint32_t)(wd >> 32) == epoch && fu_state(wd) != 0;
-        const unsigned long long mready = __ballot(ready);
-        const unsigned long long minc = __ballot(ready && fu_state(wd) == FU_INC);
-        const uint32_t nready = mready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mready);
-        const unsigned long long in_prefix = nready == 64u ? ~0ull : ((1ull << nready) - 1ull);
-        if (minc & in_prefix) {
-          const uint32_t f = (uint32_t)__builtin_ctzll(minc & in_prefix);
-          const bool take = lane <= f;
-          if (__ballot(take && fu_not_simple(wd))) {
-            ns = true;
-          } else {
-            uint32_t vb = take ? fu_bad(wd) : 0u;
-            unsigned long long vs = 0, vm = 0;
-            if (take && j >= 0) {
-              const uint32_t off = lane == f ? 2u : 0u;  // the inclusive payload of the closest inclusive
-              vs = ld_agent(&fs.pay[4 * j + off]);
-              vm = ld_agent(&fs.pay[4 * j + off + 1]);
-            }
-            ex_bad += wave_sum(vb);
-            ex_sum += wave_sum_u64(vs);
-            const unsigned long long mm = wave_max_u64(vm);
-            ex_max = mm > ex_max ? mm : ex_max;
-          }
-          break;
-        }
-        if (nready == 64u) {  // 64 aggregates: fold them and look further back
-          if (__ballot(fu_not_simple(wd))) {
-            ns = true;
-            break;
-          }
-          const unsigned long long vs = ld_agent(&fs.pay[4 * j]), vm = ld_agent(&fs.pay[4 * j + 1]);
-          ex_bad += wave_sum(fu_bad(wd));
-          ex_sum += wave_sum_u64(vs);
-          const unsigned long long mm = wave_max_u64(vm);
-          ex_max = mm > ex_max ? mm : ex_max;
-          pos -= 64;
-          continue;
-        }
-        if (++spins > FU_SPIN_MAX) {  // never expected: fail the speculation instead of hanging
-          ns = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    if (lane == 0) {
-      const uint32_t tot_bad = ex_bad + nbad;
-      if (!ns) {
-        st_agent(&fs.pay[4 * k + 2], ex_sum + bsum);
-        st_agent(&fs.pay[4 * k + 3], ex_max > bmax ? ex_max : bmax);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      st_agent(&fs.st[k], fu_word(epoch, FU_INC, ns, tot_bad));
-      sh_ex_bad = ex_bad;
-      sh_ns = ns ? 1u : 0u;
-      if (k == gridDim.x - 1) {
-        // the window's last block: its inclusive state is the window's
-        if (!ns) {
-          const uint32_t total_ins = E - tot_bad;
-          for (int32_t bb = (int32_t)w.nb; bb >= 0 && w.off[bb] == E; bb--) o.batch_base[bb] = tot_bad;
-          if (o.out_count) *o.out_count = tot_bad;
-          g->result_count = tot_bad;
-          g->base = base;
-          if (prefix_win) g->x_sorted = base + total_ins;
-          g->x_count = base + total_ins;
-          g->win_flags = 1u | (prefix_win ? 2u : 0u);
-          g->mono_prev = 1;
-          g->ovf_bound = ovf + (u128)(ex_sum + bsum);
-          const unsigned long long idm = ex_max > bmax ? ex_max : bmax;
-          if (idm > g->x_id_max) g->x_id_max = idm;
-          g->windows_applied++;
-          g->events_total += E;
-          g->w_count = 0;
-          g->cpw_want = 0;
-          g->rc_last = 0;
-          g->sp_done = 1;
-          g->sp_fails = 0;
-          g->sp_state = prefix_win ? FU_STATE_NONE : FU_STATE_INSERT;
-          g->fu_windows++;
-        } else {
-          g->sp_done = 0;
-          g->sp_state = FU_STATE_UNDO;
-          const uint32_t fails = g->sp_fails + 1;
-          g->sp_fails = fails;
-          g->sp_skip = fails >= 12 ? 4096u : (1u << fails);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (sh_ns) return;  // not simple so far: the general path rewrites everything this window
-
-  // Replies and records at their ranks (every event either fails or inserts).
-  const uint32_t rbad = sh_ex_bad + wp + inc - (bad ? 1u : 0u);
-  const uint32_t rins = i - rbad;
-  if (i < E) {
-    if (i == w.off[b]) {
-      // event i opens batch b and every empty batch just before it
-      for (int32_t bb = (int32_t)b; bb >= 0 && w.off[bb] == i; bb--) o.batch_base[bb] = rbad;
-    }
-    if (bad) {
-      tb_create_result_t r;
-      r.index = i - w.off[b];
-      r.result = fe.code;
-      o.results[rbad] = r;
-    }
-    if (ok) d.xstatus[base + rins] = 0;
-  }
-  // this wave's inserted records as one contiguous run through LDS, in two halves of 64 B
-  if (okm) {
-    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, (int)__builtin_ctzll(okm));
-    const uint32_t nins = (uint32_t)__popcll(okm);
-    const uint32_t pos = ok ? (uint32_t)__popcll(okm & ((1ull << lane) - 1ull)) : 0u;
-    uint4* ws = stage + wave * 256;
-    const uint4* src = reinterpret_cast<const uint4*>(&t);
-    uint4* dst = reinterpret_cast<uint4*>(d.xr + (base + r0));
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-      wave_sync();
-      if (ok) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) ws[pos * 4 + q] = src[half * 4 + q];
-      }
-      wave_sync();
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const uint32_t idx = c * 64 + lane, r = idx >> 2, q = idx & 3;
-        if (r < nins) st_stream(dst + r * 8 + half * 4 + q, ws[idx]);
+        const unsigned long long nv = ((unsigned long long)epoch << 32) |
+                                      (((uint32_t)(old >> 32) == epoch ? (uint32_t)old : 0u) + nbad);
+        const unsigned long long seen = atomicCAS(acc, old, nv);
+        if (seen == old) break;
+        old = seen;
       }
     }
   }
 }
 
-// After k_ct_fused (same grid): a window outside the class gets the balance adds of every block that
-// applied them subtracted (the same decisions from the same inputs); a committed window whose records
-// do not extend the sorted prefix gets its ids indexed.
-__global__ void __launch_bounds__(FU_T) k_fu_post(Dev d, FuScratch fs, const tb_transfer_t* __restrict__ ev,
-                                                  uint32_t E, uint32_t epoch) {
+// After k_ct_fused (same grid). A window outside the class: the balance adds of every block that
+// applied them are subtracted (the same decisions from the same inputs) and the general path runs.
+// A committed window: replies, batch bases, the records after the first failure moved to their ranks,
+// the ids indexed when the records do not extend the sorted prefix, and (last block) the window's
+// totals into Globals.
+__global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
+                                                   WinDesc w, uint32_t epoch, FinalOut o) {
+  __shared__ uint4 stage[FU_T * 4];
+  __shared__ uint32_t lds[FU_T / 64];
+  __shared__ unsigned long long red[2 * (FU_T / 64)];
   Globals* g = d.g;
-  if (WIN_REJECTED(g)) return;
-  const uint32_t state = g->sp_state;
-  if (state == FU_STATE_NONE) return;
-  const uint32_t k = blockIdx.x, i = k * FU_T + threadIdx.x;
-  if (state == FU_STATE_UNDO) {
+  if (WIN_REJECTED(g) || g->fu_epoch != epoch) return;  // (k_ct_fused backed off)
+  const uint32_t k = blockIdx.x, i = k * FU_T + threadIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t E = w.E;
+  if (g->fu_abort == epoch) {
+    if (k == 0 && threadIdx.x == 0) {
+      g->sp_done = 0;
+      const uint32_t fails = g->sp_fails + 1;
+      g->sp_fails = fails;
+      g->sp_skip = fails >= 12 ? 4096u : (1u << fails);
+    }
     if (!fs.applied[k] || i >= E) return;
     FuEv fe;
     fu_decide(d, ev, i, ev[i], g->x_id_max, g->x_sorted, &fe);
@@ -386,11 +282,87 @@ __global__ void __launch_bounds__(FU_T) k_fu_post(Dev d, FuScratch fs, const tb_
     }
     return;
   }
-  // FU_STATE_INSERT: ranks from the look-back's inclusive failure counts
-  __shared__ uint32_t lds[FU_T / 64];
-  const bool ok = i < E && ((fs.ok[i >> 6] >> (threadIdx.x & 63)) & 1ull);
-  const uint32_t ex_bad = k ? fu_bad(fs.st[k - 1]) : 0u;
+  const uint64_t base = g->fu_base;
+  const bool prefix_win = g->fu_prefix != 0;
+  const unsigned long long bw = g->fu_bad;
+  const uint32_t total_bad = (uint32_t)(bw >> 32) == epoch ? (uint32_t)bw : 0u;
+  // the failures of the earlier blocks (only a window with failures pays for the sum)
+  uint32_t ex_bad = 0;
+  if (total_bad) {
+    uint32_t v = 0;
+    for (uint32_t j = threadIdx.x; j < k; j += FU_T) v += fs.cnt[j];
+    ex_bad = block_sum<FU_T / 64>(v, lds);
+  }
+  const bool ok = i < E && ((fs.ok[i >> 6] >> lane) & 1ull);
+  const bool bad = i < E && !ok;
   uint32_t tot;
-  const uint32_t rb = block_excl<FU_T / 64>((i < E && !ok) ? 1u : 0u, lds, &tot);
-  if (ok) x_insert(d.x_tab, d.x_mask, ev[i].id, (uint32_t)(g->base + (i - ex_bad - rb)));
+  const uint32_t rbad = ex_bad + (total_bad ? block_excl<FU_T / 64>(bad ? 1u : 0u, lds, &tot) : 0u);
+  const uint32_t rins = i - rbad;
+  if (i < E) {
+    const uint32_t b = win_batch(w, i);
+    if (i == w.off[b]) {
+      // event i opens batch b and every empty batch just before it
+      for (int32_t bb = (int32_t)b; bb >= 0 && w.off[bb] == i; bb--) o.batch_base[bb] = rbad;
+    }
+    if (bad) {
+      tb_create_result_t r;
+      r.index = i - w.off[b];
+      r.result = s.code[i];
+      o.results[rbad] = r;
+    }
+  }
+  if (__ballot(ok && rbad != 0)) {
+    // an earlier event failed: this wave's records move down to their ranks (from the input; the
+    // branch is wave-uniform, so the run's store loop has every lane)
+    tb_transfer_t t;
+    if (ok) {
+      t = ev[i];
+      t.timestamp = win_ts(w, win_batch(w, i), i);
+      d.xstatus[base + rins] = 0;
+    }
+    const unsigned long long okm = __ballot(ok);
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, (int)__builtin_ctzll(okm));
+    fu_store_records(d, t, ok, okm, base + r0, stage + wave * 256);
+  }
+  if (ok && !prefix_win) x_insert(d.x_tab, d.x_mask, ev[i].id, (uint32_t)(base + rins));
+  if (k == gridDim.x - 1) {
+    // the window's totals: the per-block sums folded, the store counts and the window state
+    unsigned long long sum = 0, mx = 0;
+    for (uint32_t j = threadIdx.x; j < gridDim.x; j += FU_T) {
+      sum += fs.pay[2 * j];
+      mx = fs.pay[2 * j + 1] > mx ? fs.pay[2 * j + 1] : mx;
+    }
+    sum = wave_sum_u64(sum);
+    mx = wave_max_u64(mx);
+    if (lane == 0) {
+      red[2 * wave] = sum;
+      red[2 * wave + 1] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (uint32_t q = 1; q < FU_T / 64; q++) {
+        sum += red[2 * q];
+        mx = red[2 * q + 1] > mx ? red[2 * q + 1] : mx;
+      }
+      const uint32_t total_ins = E - total_bad;
+      for (int32_t bb = (int32_t)w.nb; bb >= 0 && w.off[bb] == E; bb--) o.batch_base[bb] = total_bad;
+      if (o.out_count) *o.out_count = total_bad;
+      g->result_count = total_bad;
+      g->base = base;
+      if (prefix_win) g->x_sorted = base + total_ins;
+      g->x_count = base + total_ins;
+      g->win_flags = 1u | (prefix_win ? 2u : 0u);
+      g->mono_prev = 1;
+      g->ovf_bound += (u128)sum;  // below 2^64 (glob_ok, FU_AMOUNT_MAX)
+      if (mx > g->x_id_max) g->x_id_max = mx;
+      g->windows_applied++;
+      g->events_total += E;
+      g->w_count = 0;
+      g->cpw_want = 0;
+      g->rc_last = 0;
+      g->sp_done = 1;
+      g->sp_fails = 0;
+      g->fu_windows++;
+    }
+  }
 }
