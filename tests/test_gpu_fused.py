@@ -199,3 +199,56 @@ def test_fused_equals_general_path_digest():
         a.close()
         b.close()
         ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bad_windows", [(2,), (0, 3), (5,), ()])
+def test_fused_only_windows_replayed_at_sync(bad_windows):
+    """Windows queued without a sync in between (the device-resident path, launched fused-only while
+    the stream is order-free): a window that leaves the class stops every later one on the device,
+    and tbg_sync replays it and all later windows through the general path. An accounts window in
+    the middle is replayed too. Every window's replies and the final stores equal the restatement's."""
+    import torch
+
+    from tigerbeetle_amd.state_machine import to_host
+
+    n_acc = 2000
+    gpu, ref = _engines(n_acc + 64, 1 << 19)
+    try:
+        _accounts(gpu, ref, n_acc + 2, flags={n_acc: 2, n_acc + 1: 8})
+        first, keep, outs, expect = 0, [], [], []
+        for wi in range(8):
+            if wi == 4:  # create_accounts between transfer windows
+                acc = workload.accounts(n_acc + 2, 40, seed=11)
+                op, batches = Operation.create_accounts, [acc]
+            else:
+                op, batches = Operation.create_transfers, _window(first, n_acc)
+                first += WIN * BM
+                if wi in bad_windows:
+                    ev = batches[WIN // 2]
+                    ev["flags"][100] = 2  # pending
+                    ev["timeout"][100] = 0
+                    ev["debit_account_id_lo"][200] = n_acc + 1  # the limited account
+            ns, ts = [], []
+            for ev in batches:
+                gpu.prepare_timestamp += 1 + len(ev)
+                ns.append(len(ev))
+                ts.append(gpu.prepare_timestamp)
+            data = np.concatenate([np.frombuffer(ev.tobytes(), np.uint8) for ev in batches])
+            d_ev = torch.from_numpy(data.copy()).cuda()
+            d_res = torch.zeros(max(sum(ns), 1) * 8, dtype=torch.uint8).cuda()
+            d_base = torch.zeros(len(ns) + 1, dtype=torch.int32).cuda()
+            torch.cuda.synchronize()
+            gpu.commit_window(op, d_ev.data_ptr(), ns, ts, d_res.data_ptr(), d_base.data_ptr(), True, ts[0])
+            keep.append((d_ev, d_res, d_base, len(ns)))
+            expect.append(oracle_batches(ref, op, batches))
+        gpu.sync()
+        for (d_ev, d_res, d_base, nb), r in zip(keep, expect):
+            res, base = to_host(d_res).tobytes(), to_host(d_base)
+            assert [res[base[b] * 8: base[b + 1] * 8] for b in range(nb)] == r
+        st = gpu.stats()
+        assert st["fused_windows"] >= (1 if bad_windows else 7)
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()

@@ -80,7 +80,8 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t w_count;
   // bit 0: a window was rejected whole because a pulse with expiries would fall due inside it
   // (sticky: every later window is skipped until tbg_sync reports and clears it); bit 1: sharded
-  // window outside the class; bit 2: index guard
+  // window outside the class; bit 2: index guard; bit 3: a fused-only window left the class (host.inc
+  // settle() replays it and the windows after it)
   uint32_t window_error;
   uint64_t base;  // acc_count / x_count at batch start (captured by the scan kernel)
   // pulse
@@ -144,6 +145,8 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t fu_base;     // that window's first record slot
   uint64_t fu_bad;      // that window's failures: [63:32] epoch | [31:0] count
   uint64_t fu_windows;  // cumulative windows committed by the fused pass
+  uint32_t fu_fail_epoch;  // the fused-only window that left the class (window_error bit 3)
+  uint32_t pad6;
 };
 
 // The fused pass (fused.h) committed this window: the general path's kernels return at once.
@@ -168,8 +171,10 @@ __device__ inline bool last_block_done(uint32_t* counter, uint32_t* flag_lds) {
 }
 
 // A rejected window (Globals::window_error bit 0) is skipped by every kernel that could change
-// state, and so is every window queued after it, until the host has seen the error (tbg_sync).
-#define WIN_REJECTED(g) (__builtin_expect(((g)->window_error & 1u) != 0, 0))
+// state, and so is every window queued after it, until the host has seen the error (tbg_sync). Bit 3:
+// a fused-only window left the class (fused.h): every later window is skipped until settle() replays
+// them.
+#define WIN_REJECTED(g) (__builtin_expect(((g)->window_error & 9u) != 0, 0))
 
 // Per-event class bits (scratch `cls`).
 enum : uint32_t {

@@ -257,13 +257,16 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
 // A committed window: replies, batch bases, the records after the first failure moved to their ranks,
 // the ids indexed when the records do not extend the sorted prefix, and (last block) the window's
 // totals into Globals.
+// fo_only: the general path was not launched for this window (host.inc launch_window); a window
+// outside the class then stops every later window (window_error bit 3) until the host replays them.
 __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
-                                                   WinDesc w, uint32_t epoch, FinalOut o) {
+                                                   WinDesc w, uint32_t epoch, FinalOut o, uint32_t fo_only) {
   __shared__ uint4 stage[FU_T * 4];
   __shared__ uint32_t lds[FU_T / 64];
   __shared__ unsigned long long red[2 * (FU_T / 64)];
   Globals* g = d.g;
-  if (WIN_REJECTED(g) || g->fu_epoch != epoch) return;  // (k_ct_fused backed off)
+  // (bit 0 only: this kernel itself may set bit 3, and every block must still undo its adds)
+  if ((g->window_error & 1u) || g->fu_epoch != epoch) return;  // (k_ct_fused backed off or skipped)
   const uint32_t k = blockIdx.x, i = k * FU_T + threadIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t E = w.E;
   if (g->fu_abort == epoch) {
@@ -272,6 +275,10 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
       const uint32_t fails = g->sp_fails + 1;
       g->sp_fails = fails;
       g->sp_skip = fails >= 12 ? 4096u : (1u << fails);
+      if (fo_only) {
+        g->fu_fail_epoch = epoch;
+        atomicOr(&g->window_error, 8u);
+      }
     }
     if (!fs.applied[k] || i >= E) return;
     FuEv fe;
