@@ -35,6 +35,11 @@
 #ifndef FU_EXP
 #define FU_EXP 0
 #endif
+// event loads: 0 per lane (8 strided 16 B loads), 1 staged through LDS in 64 B halves, 2 the same
+// nontemporal (the stream passes by; the account table and records stay in the Infinity Cache)
+#ifndef FU_STAGE
+#define FU_STAGE 2
+#endif
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
@@ -60,8 +65,9 @@ struct FuEv {
   bool simple, reach;
 };
 
-__device__ __forceinline__ void fu_decide(const Dev& d, const tb_transfer_t* __restrict__ ev, uint32_t i,
-                                          const tb_transfer_t& t, uint64_t x_id_max, uint64_t P, FuEv* o) {
+// prev_id_lo: the id of event i - 1 (i > 0).
+__device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, uint64_t prev_id_lo, const tb_transfer_t& t,
+                                          uint64_t x_id_max, uint64_t P, FuEv* o) {
   const uint16_t f = t.flags;
   o->dr = o->cr = NONE32;
   o->amount = 0;
@@ -69,7 +75,7 @@ __device__ __forceinline__ void fu_decide(const Dev& d, const tb_transfer_t* __r
   o->reach = false;
   // claim-free: ids strictly increasing over the window, below 2^64, no post/void (k_ct_prep's test)
   bool simple = !(f & TB_TRANSFER_LINKED) && t.id.hi == 0 && !(f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
-  if (i > 0) simple = simple && t.id.lo > ev[i - 1].id.lo;
+  if (i > 0) simple = simple && t.id.lo > prev_id_lo;
   uint32_t code;
   if (t.timestamp != 0) {
     code = TB_CT_TIMESTAMP_MUST_BE_ZERO;  // :1251
@@ -188,9 +194,41 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   fe.code = TB_CT_OK;
   fe.amount = fe.id_key = 0;
   fe.dr = fe.cr = NONE32;
+  uint64_t prev = 0;
+#if FU_STAGE
+  if (!aborted) {
+    // the wave's 64 records through LDS in two 64 B halves (16 B per lane per load, row-swizzled so
+    // the per-lane row reads are conflict-free)
+    uint4* ws = stage + wave * 256;
+    const uint32_t i0 = i - lane;
+    const uint32_t nrec = i0 < E ? min(64u, E - i0) : 0u;
+    const uint4* src = reinterpret_cast<const uint4*>(ev + i0);
+    uint4* tw = reinterpret_cast<uint4*>(&t);
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      wave_sync();
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint32_t idx = c * 64 + lane, r = idx >> 2, q = idx & 3;
+        if (r < nrec) ws[r * 4 + (q ^ ((r >> 2) & 3))] = FU_STAGE == 2 ? ld_stream(src + r * 8 + half * 4 + q)
+                                                                        : src[r * 8 + half * 4 + q];
+      }
+      wave_sync();
+#pragma unroll
+      for (int q = 0; q < 4; q++) tw[half * 4 + q] = ws[lane * 4 + (q ^ ((lane >> 2) & 3))];
+    }
+    // the previous event's id: the neighbour lane's (lane 0: the previous wave's last event)
+    prev = __shfl_up(t.id.lo, 1, 64);
+    if (lane == 0 && i > 0) prev = ev[i - 1].id.lo;
+  }
+#else
   if (i < E && !aborted) {
     t = ev[i];
-    fu_decide(d, ev, i, t, x_id_max, P, &fe);
+    if (i > 0) prev = ev[i - 1].id.lo;
+  }
+#endif
+  if (i < E && !aborted) {
+    fu_decide(d, i, prev, t, x_id_max, P, &fe);
     t.timestamp = win_ts(w, win_batch(w, i), i);  // :1253 (the record as inserted)
   }
   const bool blk_simple = __syncthreads_and(fe.simple) && glob_ok && !aborted;
@@ -282,7 +320,7 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
     }
     if (!fs.applied[k] || i >= E) return;
     FuEv fe;
-    fu_decide(d, ev, i, ev[i], g->x_id_max, g->x_sorted, &fe);
+    fu_decide(d, i, i > 0 ? ev[i - 1].id.lo : 0ull, ev[i], g->x_id_max, g->x_sorted, &fe);
     if (fe.code == TB_CT_OK) {
       (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.dr].debits_posted), 0ull - fe.amount);
       (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.cr].credits_posted), 0ull - fe.amount);
@@ -293,6 +331,11 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
   const bool prefix_win = g->fu_prefix != 0;
   const unsigned long long bw = g->fu_bad;
   const uint32_t total_bad = (uint32_t)(bw >> 32) == epoch ? (uint32_t)bw : 0u;
+  if (!total_bad && prefix_win && k != gridDim.x - 1) {
+    // nothing moves, nothing to index: only a block where a batch starts has a reply base to write
+    const uint32_t lo = k * FU_T, hi = min(E, lo + FU_T), b = win_batch(w, lo);
+    if (w.off[b] != lo && !(b + 1 < w.nb && w.off[b + 1] < hi)) return;
+  }
   // the failures of the earlier blocks (only a window with failures pays for the sum)
   uint32_t ex_bad = 0;
   if (total_bad) {
