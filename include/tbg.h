@@ -119,7 +119,12 @@ int tbg_commit_device(tbg_engine *engine, uint32_t operation, uint64_t timestamp
  * window in which a pulse with expiries would fall due is rejected whole (its pulse included). A
  * rejected window skips every window queued after it too: tbg_sync() returns TBG_E_WINDOW and
  * tbg_windows_committed() tells how many windows were applied; resubmitting the same batches is
- * exact. Asynchronous on the engine stream. n_batches <= 128, total events <= window_events_max. */
+ * exact. Asynchronous on the engine stream. n_batches <= 128, total events <= window_events_max.
+ * An order-free transfer window (plain creates between unlimited accounts, ids strictly increasing)
+ * is committed by the one-pass fused kernels (csrc/fused.h); while a stream stays order-free its
+ * windows launch nothing else, and a window that turns out not to be is re-run through the general
+ * path at the next tbg_sync (or any call that reads state). So d_events, d_results and d_batch_base
+ * must stay valid until tbg_sync returns. */
 int tbg_commit_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_batches,
                       const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_results,
                       uint32_t *d_batch_base, int auto_pulse, uint64_t prepare_timestamp);
