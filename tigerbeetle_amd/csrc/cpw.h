@@ -76,7 +76,8 @@ __global__ void __launch_bounds__(256) k_cc_keys(Dev d, Scratch s, uint32_t E) {
   s.rval_in[i] = i;
 }
 
-// Component starts in the sorted order.
+// Component starts in the sorted order, and each component's last sorted position by root
+// (Scratch::light: no resolver runs in a component-walked window).
 // One counter atomic per 1024-thread block: same-address atomics serialize at the memory side
 // (~140K component starts in a cfg4 window; even one per wave cost ~90 us).
 __global__ void __launch_bounds__(1024) k_cc_segs(Dev d, Scratch s, uint32_t E) {
@@ -88,6 +89,7 @@ __global__ void __launch_bounds__(1024) k_cc_segs(Dev d, Scratch s, uint32_t E) 
   if (k < E) {
     const uint32_t key = s.rkey[k];
     start = key != RES_DUMMY && (k == 0 || s.rkey[k - 1] != key);
+    if (key != RES_DUMMY && (k + 1 == E || s.rkey[k + 1] != key)) s.light[key] = k;  // (root < E)
   }
   uint32_t tot;
   const uint32_t r = block_excl<1024 / 64>(start ? 1u : 0u, lds, &tot);
@@ -97,20 +99,20 @@ __global__ void __launch_bounds__(1024) k_cc_segs(Dev d, Scratch s, uint32_t E) 
   if (start) s.cc_list[base + r] = k;
 }
 
-// One walker per component: events rval[start .. start + len), undo records from 5 * start.
+// One walker per component: events rval[start .. start + len), undo records from 5 * start (the
+// length from the component's last sorted position, k_cc_segs: no scan of the sorted keys).
 template <bool XFER>
 __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t* ev, WinDesc w, uint32_t epoch) {
   Globals* g = d.g;
   if (!cpw_active(g)) return;
+  __shared__ uint2 pcache[256 * WCACHE];
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j == 0) g->cpw_done = 1;
   const bool on = j < g->cc_count;
   uint32_t start = 0, len = 0;
   if (on) {
     start = s.cc_list[j];
-    const uint32_t key = s.rkey[start];
-    len = 1;
-    while (start + len < w.E && s.rkey[start + len] == key) len++;
+    len = s.light[s.rkey[start]] + 1 - start;
   }
   // statistics (tbg_debug_counters): [5] longest component, [6] components, [7] W events walked;
   // one lane per block adds (same-address atomics from every wave serialize at the memory side)
@@ -137,7 +139,6 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
     atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)st_sum);
   }
   if (!on) return;
-  __shared__ uint2 pcache[256 * WCACHE];
   uint2* mine = pcache + threadIdx.x * WCACHE;
   for (int k = 0; k < WCACHE; k++) mine[k] = make_uint2(NONE32, 0);
   Walker wk;

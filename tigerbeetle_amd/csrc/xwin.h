@@ -146,17 +146,26 @@ __global__ void __launch_bounds__(256) k_xwin_minlive(Dev d, Scratch s, WinDesc 
 __global__ void __launch_bounds__(XW_THREADS) k_xwin_replay(Dev d, Scratch s, WinDesc w) {
   __shared__ unsigned long long ldsm[XW_THREADS / 64];
   __shared__ uint32_t first_eff;
+  // the per-batch tables in LDS (one coalesced load), so the batch-by-batch walk below pays no
+  // dependent global load per batch (the segment-tree path alone was 8 of them)
+  __shared__ unsigned long long tree[2 * MAXB], minx[MAXB], miny[MAXB];
   if (WIN_REJECTED(d.g)) return;
+  for (uint32_t j = threadIdx.x; j < 2 * MAXB; j += XW_THREADS) tree[j] = s.xw_tree[j];
+  for (uint32_t j = threadIdx.x; j < MAXB; j += XW_THREADS) {
+    minx[j] = s.xw_minx[j];
+    miny[j] = s.xw_miny[j];
+  }
+  __syncthreads();
   uint64_t pn = d.g->pulse_next;  // after the window's first pulse
   for (uint32_t b = 0; b < w.nb; b++) {
     if (b >= 1 && pn <= w.T[b]) {
       // the pulse before batch b: its finish takes the smallest entry live after it
       unsigned long long m = ~0ull;
-      for (uint32_t node = MAXB + b; node >= 1; node >>= 1) m = umin64(m, s.xw_tree[node]);
+      for (uint32_t node = MAXB + b; node >= 1; node >>= 1) m = umin64(m, tree[node]);
       pn = m == ~0ull ? TB_TIMESTAMP_MAX : m;
     }
-    if (s.xw_miny[b] > pn) {  // no reset can take effect (it needs expires_at == pulse_next <= pn)
-      pn = umin64(pn, s.xw_minx[b]);
+    if (miny[b] > pn) {  // no reset can take effect (it needs expires_at == pulse_next <= pn)
+      pn = umin64(pn, minx[b]);
       continue;
     }
     bool reset = false;
