@@ -159,8 +159,9 @@ void *tbg_stream(tbg_engine *engine);
  * receives the same window (same arguments as tbg_commit_window) and is the home of a contiguous
  * range of its batches (it decides them and writes their replies):
  *   1. tbg_shard_prepare_window: validates and resolves what it owns (accounts, transfer ids) and
- *      writes tbg_shard_exchange_bytes(operation, E) bytes of owner facts at d_exchange (16 B trailer,
- *      then 9 B per create_transfers event / 1 B per create_accounts event);
+ *      writes tbg_shard_exchange_bytes(operation, E, G) bytes of owner facts at d_exchange (16 B
+ *      trailer, then 2 B per create_transfers event plus G x 4096 ledger-mismatch slots of 8 B /
+ *      1 B per create_accounts event);
  *   2. the caller sums those bytes element-wise across all G shards in place, ordered on the engine
  *      stream (ncclAllReduce(uint8, ncclSum) over xGMI, e.g. torch.distributed.all_reduce); every bit
  *      has exactly one writer, so the byte-wise sum is exact;
@@ -175,7 +176,7 @@ void *tbg_stream(tbg_engine *engine);
  * in-window duplicate ids, overflow-free. Any other window is rejected whole on every shard:
  * tbg_sync returns TBG_E_UNSUPPORTED and no shard has applied it. Asynchronous on the engine stream. */
 uint32_t tbg_shard_of(uint64_t id_lo, uint64_t id_hi, uint32_t shard_count);
-uint64_t tbg_shard_exchange_bytes(uint32_t operation, uint32_t n_events);
+uint64_t tbg_shard_exchange_bytes(uint32_t operation, uint32_t n_events, uint32_t shard_count);
 uint64_t tbg_shard_commit_bits_bytes(uint32_t n_events);
 int tbg_shard_prepare_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_batches,
                              const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_exchange);

@@ -129,7 +129,7 @@ def lib():
         "tbg_shard_commit_window": ([vp, vp, vp], i32),
         "tbg_shard_commit_bits_bytes": ([u32], u64),
         "tbg_window_changes": ([vp, vp, u64, P(u64), vp, u64, P(u64), vp, u64, P(u64)], i32),
-        "tbg_shard_exchange_bytes": ([u32, u32], u64),
+        "tbg_shard_exchange_bytes": ([u32, u32, u32], u64),
         "tbg_windows_committed": ([vp, P(u64), P(u64)], i32),
         "tbg_open": ([vp, vp, u64, vp, u64, vp, vp, u64], i32),
         "tbg_reset": ([vp], i32),

@@ -146,7 +146,7 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t fu_bad;      // that window's failures: [63:32] epoch | [31:0] count
   uint64_t fu_windows;  // cumulative windows committed by the fused pass
   uint32_t fu_fail_epoch;  // the fused-only window that left the class (window_error bit 3)
-  uint32_t pad6;
+  uint32_t sh_mis;         // sharded: this shard's ledger-mismatch slots used this window (shard.h)
 };
 
 // The fused pass (fused.h) committed this window: the general path's kernels return at once.

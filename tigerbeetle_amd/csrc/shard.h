@@ -39,35 +39,57 @@
 #include "walker.h"
 #include "window.h"
 
-// Exchange bytes of a window of E events (summed byte-wise over the shards: every bit has exactly
-// one writer, so the byte sum is the union with no carries; one uint8 all-reduce):
-//   [0, 16)         trailer, 4 x u32: shards that saw an unsupported event, shards over capacity,
-//                   shards whose overflow bound does not clear the window's amounts, unused
+// Exchange bytes of a window of E events over G shards (summed byte-wise over the shards: every bit
+// has exactly one writer, so the byte sum is the union with no carries; one uint8 all-reduce):
+//   [0, 16)         trailer, 4 x u32: shards that saw an unsupported event (or overflowed their
+//                   ledger-mismatch slots), shards over capacity, shards whose overflow bound does not
+//                   clear the window's amounts, unused
+//   [16, 16+E)      bits 0-5: 1 + (TB_CT_OK or the exists* code; create_accounts: 1 + the code), by
+//                   the id owner; bit 6: the debit account has debits_must_not_exceed_credits or
+//                   flags.history (its owner); bit 7: the credit account has
+//                   credits_must_not_exceed_debits or flags.history (its owner)
 //   create_transfers:
-//   [16, 16+4E)     debit account's ledger (its owner; 0 = not found: a live ledger is never 0, :1436)
-//   [16+4E, 16+8E)  credit account's ledger
-//   [16+8E, 16+9E)  bits 0-5: 1 + (TB_CT_OK or the exists* code), by the transfer-id owner;
-//                   bit 6: the debit account has debits_must_not_exceed_credits or flags.history
-//                   (its owner); bit 7: the credit account has credits_must_not_exceed_debits or
-//                   flags.history (its owner)
-//   create_accounts:
-//   [16, 16+E)      bits 0-5: 1 + the id owner's code
+//   [16+E, 16+2E)   the account sides' states (SH_ACC_*): bits 0-1 the debit account, 2-3 the credit
+//                   account, each by its owner against the event's ledger
+//   [16+2E, ...)    G x SH_MIS_SLOTS u64 ledger-mismatch slots, shard g's at [g * SH_MIS_SLOTS, ...):
+//                   valid << 63 | side << 52 | event << 32 | the account's ledger
+// A side's ledger is needed only when both accounts mismatch the event's ledger (then whether they
+// match each other decides between accounts_must_have_the_same_ledger and
+// transfer_must_have_the_same_ledger_as_accounts, :1503-1504), so the 8 B of ledgers per event of the
+// first protocol are 2 bits of state per side plus rare mismatch slots: 2 B per event instead of 9.
 enum : uint32_t { SH_Z_MASK = 0x3F, SH_DR_LIMIT = 0x40, SH_CR_LIMIT = 0x80 };
+enum : uint32_t { SH_ACC_OK = 1, SH_ACC_MISSING = 2, SH_ACC_MISMATCH = 3 };
+#define SH_MIS_SLOTS 4096u  // per shard; more mismatches in one window: outside the class (trailer 0)
 
 struct XchView {
   uint32_t* trailer;
-  uint32_t *drl, *crl;  // transfers only
   uint8_t* zw;
+  uint8_t* acc;              // transfers only
+  unsigned long long* mis;   // transfers only: G x SH_MIS_SLOTS
+  uint32_t G;
 };
-__host__ __device__ inline uint64_t xch_bytes(bool xfer, uint32_t E) { return 16 + (xfer ? 9ull : 1ull) * E; }
-__host__ __device__ inline XchView xch_view(void* base, uint32_t E, bool xfer) {
+__host__ __device__ inline uint64_t xch_mis_off(uint32_t E) { return (16 + 2ull * E + 7) & ~7ull; }
+__host__ __device__ inline uint64_t xch_bytes(bool xfer, uint32_t E, uint32_t G) {
+  return xfer ? xch_mis_off(E) + 8ull * G * SH_MIS_SLOTS : 16 + (uint64_t)E;
+}
+__host__ __device__ inline XchView xch_view(void* base, uint32_t E, bool xfer, uint32_t G) {
   uint8_t* p = reinterpret_cast<uint8_t*>(base);
   XchView v;
   v.trailer = reinterpret_cast<uint32_t*>(p);
-  v.drl = xfer ? reinterpret_cast<uint32_t*>(p + 16) : nullptr;
-  v.crl = xfer ? reinterpret_cast<uint32_t*>(p + 16 + 4ull * E) : nullptr;
-  v.zw = p + 16 + (xfer ? 8ull * E : 0ull);
+  v.zw = p + 16;
+  v.acc = xfer ? p + 16 + E : nullptr;
+  v.mis = xfer ? reinterpret_cast<unsigned long long*>(p + xch_mis_off(E)) : nullptr;
+  v.G = G;
   return v;
+}
+// A side's ledger from the mismatch slots (both sides mismatched; never expected to be missing).
+__device__ inline uint32_t xch_mis_ledger(const XchView& x, uint32_t e, uint32_t side) {
+  const unsigned long long want = (1ull << 63) | ((unsigned long long)side << 52) | ((unsigned long long)e << 32);
+  for (uint32_t k = 0; k < x.G * SH_MIS_SLOTS; k++) {
+    const unsigned long long v = x.mis[k];
+    if ((v & 0xFFFFFFFF00000000ull) == want) return (uint32_t)v;
+  }
+  return 0;
 }
 
 // Guard on every computed index of the sharded path: a violation is recorded (first one wins:
@@ -265,10 +287,13 @@ __global__ void __launch_bounds__(SEG) k_sh_roles(Dev d, Scratch s, const uint8_
       if (i > 0) nm |= !(id.lo > reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i - 1].id.lo);
       if (nm) atomicOr(&aux, (uint32_t)SHX_NONMONO);
       if (i == 0 && id.hi == 0 && id.lo > d.g->x_id_max) atomicOr(&aux, (uint32_t)SHX_FRESH);
-      xch.drl[i] = 0;  // k_sh_owned writes the owned facts
-      xch.crl[i] = 0;
+      xch.acc[i] = 0;  // k_sh_owned writes the owned facts
     }
     xch.zw[i] = 0;
+  }
+  if (XFER) {  // the mismatch slots (every shard's, zero but its own writes) and this shard's count
+    for (uint32_t k = i; k < G * SH_MIS_SLOTS; k += gridDim.x * SEG) xch.mis[k] = 0;
+    if (i == 0) d.g->sh_mis = 0;
   }
   uint32_t tot;
   const uint32_t r = block_excl<SEG / 64>(roles ? 1u : 0u, lds, &tot);
@@ -297,7 +322,7 @@ __device__ inline void check_window(const WinDesc& w, Globals* g) {
 
 // ones that carry effects.
 __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
-                                                     uint32_t epoch, XchView xch) {
+                                                     uint32_t epoch, XchView xch, uint32_t me) {
   __shared__ u128 red[SEG / 64];
   __shared__ uint32_t aux;
   const uint32_t k = blockIdx.x * SEG + threadIdx.x;
@@ -340,34 +365,37 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
     if (cand & (ROLE_DR | ROLE_CR)) {
       const uint4* q = reinterpret_cast<const uint4*>(ev + i);
       const uint4 q1 = q[1], q2 = q[2], q3 = q[3];
+      const uint32_t ledger = q[7].x;  // the event's ledger: each side's state is against it
       amount_upper = U(rw_u128(q3));
+      uint32_t acc = 0;
       // up to two independent probes, one per owned side
-      if (cand & ROLE_DR) {
-        roles |= ROLE_DR;
+#pragma unroll
+      for (uint32_t side = 0; side < 2; side++) {
+        if (!(cand & (side ? ROLE_CR : ROLE_DR))) continue;
+        roles |= side ? ROLE_CR : ROLE_DR;
         AccEntry e;
-        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, rw_u128(q1), &e);
-        s.dr_slot[i] = slot;
-        uint32_t drl = 0;
+        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, rw_u128(side ? q2 : q1), &e);
+        (side ? s.cr_slot : s.dr_slot)[i] = slot;
+        uint32_t st = SH_ACC_MISSING;
         if (slot != NONE32) {
-          drl = e.ledger;
+          st = e.ledger == ledger ? SH_ACC_OK : SH_ACC_MISMATCH;
           // a limit (a balance read) or flags.history (a historical_balance row of balances after
           // the event, :1806-1841): outside the order-free class if the event commits
-          if (e.flags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS | TB_ACCOUNT_HISTORY)) zw |= SH_DR_LIMIT;
+          const uint16_t lim = side ? TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS : TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS;
+          if (e.flags & (lim | TB_ACCOUNT_HISTORY)) zw |= side ? SH_CR_LIMIT : SH_DR_LIMIT;
+          if (st == SH_ACC_MISMATCH) {
+            const uint32_t k2 = atomicAdd(&d.g->sh_mis, 1u);
+            if (k2 < SH_MIS_SLOTS)
+              xch.mis[me * SH_MIS_SLOTS + k2] = (1ull << 63) | ((unsigned long long)side << 52) |
+                                                ((unsigned long long)i << 32) | e.ledger;
+            else
+              atomicOr(&aux, (uint32_t)SHX_DUP);  // (trailer 0: outside the class)
+          }
         }
-        xch.drl[i] = drl;
+        acc |= st << (2 * side);
       }
-      if (cand & ROLE_CR) {
-        roles |= ROLE_CR;
-        AccEntry e;
-        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, rw_u128(q2), &e);
-        s.cr_slot[i] = slot;
-        uint32_t crl = 0;
-        if (slot != NONE32) {
-          crl = e.ledger;
-          if (e.flags & (TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS | TB_ACCOUNT_HISTORY)) zw |= SH_CR_LIMIT;
-        }
-        xch.crl[i] = crl;
-      }
+      if (acc) xch.acc[i] = (uint8_t)acc;  // (one byte per event: both sides' owners write it only
+                                           // when they are the same shard, else their bit pairs)
     }
     if (zw) xch.zw[i] = (uint8_t)zw;
     s.wlist[k] = i | (roles << 24);
@@ -461,12 +489,16 @@ __device__ inline uint32_t sh_code(const Scratch& s, const uint8_t* ev, const Xc
   const uint32_t zw = xch.zw[j];
   const uint32_t z = (zw & SH_Z_MASK) - 1;
   if (!XFER) return z;
-  const uint32_t drl = xch.drl[j], crl = xch.crl[j];
-  if (drl == 0) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;  // :1496-1497
-  if (crl == 0) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
-  if (drl != crl) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;  // :1503-1504
-  if (reinterpret_cast<const tb_transfer_t*>(ev)[j].ledger != drl)
+  const uint32_t acc = xch.acc[j], dst = acc & 3u, cst = (acc >> 2) & 3u;
+  if (dst == SH_ACC_MISSING) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;  // :1496-1497
+  if (cst == SH_ACC_MISSING) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
+  // :1503-1504 from the states against the event's ledger: one side off it means the accounts
+  // differ; both off it, their own ledgers decide
+  if (dst == SH_ACC_MISMATCH || cst == SH_ACC_MISMATCH) {
+    if (dst != cst) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (xch_mis_ledger(xch, j, 0) != xch_mis_ledger(xch, j, 1)) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
     return TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+  }
   if (z != TB_CT_OK) return z;  // exists* (:1506-1507)
   // Reaches the balance checks: overflow cannot fail in a class window; a limit flag on either
   // account is a balance read (:1546-1547), and flags.history a row of balances after the event

@@ -99,7 +99,10 @@ class ShardedStateMachine:
         self.exchange = exchange
         events_max = window_events_max or batch_max
         dev = torch.device("cuda", device)
-        self.xch = torch.zeros(16 + 9 * events_max, dtype=torch.uint8, device=dev)
+        L = _lib.lib()
+        xb = max(L.tbg_shard_exchange_bytes(int(op), events_max, shard_count)
+                 for op in (Operation.create_accounts, Operation.create_transfers))
+        self.xch = torch.zeros(int(xb), dtype=torch.uint8, device=dev)
         self.bits = torch.zeros(int(_lib.lib().tbg_shard_commit_bits_bytes(events_max)), dtype=torch.uint8, device=dev)
         self.stream = torch.cuda.ExternalStream(self.sm.stream, device=dev)
         self._n_events = 0
@@ -126,7 +129,7 @@ class ShardedStateMachine:
         _lib.check(_lib.lib().tbg_shard_prepare_window(self.sm.h, int(operation), d_events, nb, ev, ts,
                                                        self.xch.data_ptr()), "shard_prepare_window")
         self._n_events = sum(batch_events)
-        n = _lib.lib().tbg_shard_exchange_bytes(int(operation), self._n_events)
+        n = _lib.lib().tbg_shard_exchange_bytes(int(operation), self._n_events, self.shard_count)
         return self.xch[:n]
 
     def decide_window(self, home_first, home_count, d_results, d_batch_base):

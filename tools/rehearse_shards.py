@@ -124,7 +124,7 @@ def main():
                                 "commit_mean": round(float(t[:, :, 2].mean()), 4),
                                 "max_shard_mean": round(float(per_shard.max(axis=1).mean()), 4)},
         "estimated_rate_excl_collective": round(events / crit, 1),
-        "exchange_bytes_per_window": 16 + 9 * win * BATCH + 16 + win * BATCH // 8,
+        "exchange_bytes_per_window": (16 + 2 * win * BATCH + 8 * G * 4096) + 16 + win * BATCH // 8,
         "stats_shard0": shards[0].stats(),
     }
     print(json.dumps(out), flush=True)
