@@ -148,7 +148,7 @@ def parse():
     p.add_argument("--host-fed-transfers", type=int, default=None,
                    help="cfg1/cfg2: after the timed run, commit this many further transfers of the same stream "
                         "from pinned host memory (tbg_commit_window_host, H2D overlapped with compute) and report "
-                        "it as `host_fed` (never `value`); default 8 windows, 0 = off")
+                        "it as `host_fed` (never `value`); default 32 windows (the pipeline fill, one unoverlapped H2D, is 1/32 of it), 0 = off")
     p.add_argument("--id-order", default="sequential", choices=["sequential", "random", "reversed"],
                    help="account and transfer ids as the reference benchmark's --id-order (cli.zig:97, 263-265; "
                         "testing/id.zig IdPermutation; random = pseudo-UUIDs from Xoshiro256, the reference's own ids "
@@ -166,7 +166,7 @@ def parse():
     if a.warmup is None:
         a.warmup = 256 if a.config == "cfg2" else 32
     if a.host_fed_transfers is None:
-        a.host_fed_transfers = 8 * min(a.window, WINDOW_BATCHES_MAX) * BATCH if a.config in ("cfg1", "cfg2") else 0
+        a.host_fed_transfers = 32 * min(a.window, WINDOW_BATCHES_MAX) * BATCH if a.config in ("cfg1", "cfg2") else 0
     a.tick = c["tick"]
     from tigerbeetle_amd import workload
 
