@@ -257,82 +257,97 @@ __device__ inline int32_t wave_incl_scan_i32(int32_t x) {
   return x;
 }
 
+// One 64-entry step of rc_walk_wave32 from its (already loaded) inputs; advances D.
+__device__ __attribute__((always_inline)) inline void rc_step32(RcLds& L, uint32_t k, uint32_t s1, int lane, int64_t A0,
+                                                                int64_t& D, uint32_t em, int32_t amt, uint32_t oth,
+                                                                uint64_t& rounds, uint64_t* tp) {
+  const uint64_t q0 = RC_PROF == 1 ? clock64() : 0;
+  const uint32_t kk = k + (uint32_t)lane;
+  const bool act = kk < s1;
+  const uint32_t n = min(64u, s1 - k);
+  const bool check = em & RC_EM_CHECK;
+  bool ok = act && oth != 0u;
+  int32_t eff = 0;
+  if (ok) eff = check ? -amt : ((em & RC_EM_ADD) ? amt : 0);
+  int32_t pre = wave_incl_scan_i32(eff) - eff;
+  // B = A0 + D clamped into int32 with 32-bit scalar operations (|A0| <= 2^62, |D| < 2^62)
+  const int64_t B64 = A0 + D;
+  const uint32_t blo = (uint32_t)B64;
+  const int32_t bhi = (int32_t)(B64 >> 32);
+  const int32_t B = bhi == ((int32_t)blo >> 31) ? (int32_t)blo : (bhi < 0 ? INT32_MIN : INT32_MAX);
+  // Failures in lane order: every lane after the last failure found sees the failed amounts so far
+  // added back, so the next failure is the first later candidate with amount - pre > B + acc (a
+  // uniform threshold: one compare, one find-first and one readlane per failure); the failed
+  // amounts are added to the later prefixes once, by a scan, after the last one.
+  const int32_t x = amt - pre;
+  uint64_t q1 = 0;
+  if (RC_PROF == 1) {
+    q1 = clock64();
+    tp[0] += q1 - q0;
+  }
+  const unsigned long long cand = __ballot(ok && check);
+  unsigned long long fails = 0, after = ~0ull;
+  const uint32_t room = (uint32_t)INT32_MAX - (uint32_t)B;  // B + acc stays an int32 below it
+  uint32_t acc = 0;
+  while (acc < room) {
+    const unsigned long long fm = __ballot(x > B + (int32_t)acc) & cand & after;
+    if (!fm) break;
+    const int jl = __builtin_ctzll(fm);
+    if (RC_PROF == 1) rounds++;
+    acc += (uint32_t)__builtin_amdgcn_readlane(amt, jl);
+    fails |= 1ull << jl;
+    after = jl == 63 ? 0ull : ~0ull << (jl + 1);
+  }
+  if (fails) {
+    const bool failed = (fails >> lane) & 1ull;
+    const int32_t fa = failed ? amt : 0;
+    pre += wave_incl_scan_i32(fa) - fa;
+    if (failed) eff = 0;
+  }
+  if (RC_PROF == 1) tp[1] += clock64() - q1;
+  if (act) {
+    if (check) L.cur[em & RC_EM_IDX] = amt - pre <= B ? 1 : 0;
+    L.dent[kk] = D + pre;
+  }
+  D += __builtin_amdgcn_readlane(pre + eff, (int)n - 1);
+}
+
 // Whole-wave walk of a segment whose amounts are all below 2^24 (the chunk's common case): the
 // in-step prefix and amount - prefix fit an int32 (|.| < 65 * 2^24), and a check fails iff
 // amount - pre > A0 + D, with A0 + D clamped into int32 without changing any comparison. Same
 // outputs as rc_walk_wave.
-
+// Each step's LDS inputs are loaded one step ahead into one of two register sets, alternating (the
+// loop is unrolled by two): with a single set the loop-carried copy of the prefetched values at the
+// end of each step waited for the loads it had just issued (and for the step's stores).
 __device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, int lane, uint64_t& rounds,
                                       uint64_t* tp) {
+  const uint64_t e0 = RC_PROF == 2 ? clock64() : 0;
   const uint32_t s0 = rc_uniform(L.seg[sg]), s1 = rc_uniform(L.seg[sg + 1]);
   const int64_t A0 = rc_uniform64(L.A[L.rank[s0]]);
   // a re-walk starts at the first entry whose input changed, from the balance kept before it
   int64_t D = kf == s0 ? 0 : rc_uniform64(L.dent[kf]);
-  // the step's LDS inputs are loaded one step ahead (no step's stores touch them), kept raw until
-  // used (converting a prefetched value at once would wait for its load)
-  uint32_t kk = kf + (uint32_t)lane;
-  uint32_t em_n = kk < s1 ? L.em[kk] : 0u;
-  int32_t amt_n = kk < s1 ? (int32_t)L.amt[kk] : 0;
-  uint32_t oth_n = L.oth[kk & (RC_ME - 1)];
-  for (uint32_t k = kf; k < s1; k += 64) {
-    const uint64_t q0 = RC_PROF ? clock64() : 0;
-    kk = k + (uint32_t)lane;
-    const bool act = kk < s1;
-    const uint32_t n = min(64u, s1 - k);
-    const uint32_t em = em_n;
-    const int32_t amt = amt_n;
-    const bool opass = oth_n != 0u;
-    if (k + 64u < s1) {
-      const uint32_t kn = kk + 64u;
-      em_n = kn < s1 ? L.em[kn] : 0u;
-      amt_n = kn < s1 ? (int32_t)L.amt[kn] : 0;
-      oth_n = L.oth[kn & (RC_ME - 1)];
-    }
-    const bool check = em & RC_EM_CHECK;
-    bool ok = act && opass;
-    int32_t eff = 0;
-    if (ok) eff = check ? -amt : ((em & RC_EM_ADD) ? amt : 0);
-    int32_t pre = wave_incl_scan_i32(eff) - eff;
-    // B = A0 + D clamped into int32 with 32-bit scalar operations (|A0| <= 2^62, |D| < 2^62)
-    const int64_t B64 = A0 + D;
-    const uint32_t blo = (uint32_t)B64;
-    const int32_t bhi = (int32_t)(B64 >> 32);
-    const int32_t B = bhi == ((int32_t)blo >> 31) ? (int32_t)blo : (bhi < 0 ? INT32_MIN : INT32_MAX);
-    // Failures in lane order: every lane after the last failure found sees the failed amounts so far
-    // added back, so the next failure is the first later candidate with amount - pre > B + acc (a
-    // uniform threshold: one compare, one find-first and one readlane per failure); the failed
-    // amounts are added to the later prefixes once, by a scan, after the last one.
-    const int32_t x = amt - pre;
-    uint64_t q1 = 0;
-    if (RC_PROF) {
-      q1 = clock64();
-      tp[0] += q1 - q0;
-    }
-    const unsigned long long cand = __ballot(ok && check);
-    unsigned long long fails = 0, after = ~0ull;
-    const uint32_t room = (uint32_t)INT32_MAX - (uint32_t)B;  // B + acc stays an int32 below it
-    uint32_t acc = 0;
-    while (acc < room) {
-      const unsigned long long fm = __ballot(x > B + (int32_t)acc) & cand & after;
-      if (!fm) break;
-      const int jl = __builtin_ctzll(fm);
-      if (RC_PROF) rounds++;
-      acc += (uint32_t)__builtin_amdgcn_readlane(amt, jl);
-      fails |= 1ull << jl;
-      after = jl == 63 ? 0ull : ~0ull << (jl + 1);
-    }
-    if (fails) {
-      const bool failed = (fails >> lane) & 1ull;
-      const int32_t fa = failed ? amt : 0;
-      pre += wave_incl_scan_i32(fa) - fa;
-      if (failed) eff = 0;
-    }
-    if (RC_PROF) tp[1] += clock64() - q1;
-    if (act) {
-      if (check) L.cur[em & RC_EM_IDX] = amt - pre <= B ? 1 : 0;
-      L.dent[kk] = D + pre;
-    }
-    D += __builtin_amdgcn_readlane(pre + eff, (int)n - 1);
+  if (RC_PROF == 2) {  // walks and their set-up cycles
+    rounds++;
+    tp[1] += clock64() - e0;
+  }
+  // prefetches are unconditional loads of clamped positions (lanes past the end ignore what they
+  // read): a load issued on one path only made the compiler wait for every outstanding LDS op
+  uint32_t kk = min(kf + (uint32_t)lane, (uint32_t)RC_ME - 1u);
+  uint32_t emA = L.em[kk], emB;
+  int32_t amtA = reinterpret_cast<const int32_t*>(L.amt)[2 * kk], amtB;  // the low word (< 2^24)
+  uint32_t othA = L.oth[kk], othB;
+  for (uint32_t k = kf; k < s1; k += 128) {
+    kk = min(k + 64u + (uint32_t)lane, (uint32_t)RC_ME - 1u);
+    emB = L.em[kk];
+    amtB = reinterpret_cast<const int32_t*>(L.amt)[2 * kk];
+    othB = L.oth[kk];
+    rc_step32(L, k, s1, lane, A0, D, emA, amtA, othA, rounds, tp);
+    if (k + 64u >= s1) break;
+    kk = min(k + 128u + (uint32_t)lane, (uint32_t)RC_ME - 1u);
+    emA = L.em[kk];
+    amtA = reinterpret_cast<const int32_t*>(L.amt)[2 * kk];
+    othA = L.oth[kk];
+    rc_step32(L, k + 64u, s1, lane, A0, D, emB, amtB, othB, rounds, tp);
   }
   if (lane == 0) L.delta[sg] = D;
 }
@@ -422,7 +437,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   // RC_PROF (thread 0): setup, walk phase, change detection cycles, sum of the longest wave walk per
   // iteration; per wave: load+scan and failure-search cycles, failure rounds
   uint64_t prof[4] = {0, 0, 0, 0};
-  uint64_t wrounds = 0, wt[2] = {0, 0}, hz[4] = {0, 0, 0, 0};  // RC_PROF: huge walks (cycles, steps) it 0 / later
+  uint64_t wrounds = 0, wt[2] = {0, 0}, hz[4] = {0, 0, 0, 0};  // RC_PROF > 1: head walks, other huge walks (cycles, steps)
   for (uint32_t r = t; r < R; r += RC_T) L.A[r] = rc_clamp(s.rstate[r].A);
   for (uint32_t c = t; c < nch; c += RC_T) L.cb[c] = s.rc_cb[c];  // chunk ends (k_rc_build)
   __syncthreads();
@@ -518,12 +533,18 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
         const uint32_t kf = rc_uniform(L.dfrom[H]);
         if (kf != RC_NONE) {
           L.dfrom[H] = RC_NONE;
+          const uint64_t th0 = RC_PROF ? clock64() : 0;
           __builtin_amdgcn_s_setprio(3);
           if (big) rc_walk_wave(L, H, kf, lane);
           else rc_walk_wave32(L, H, kf, lane, wrounds, wt);
           __builtin_amdgcn_s_setprio(0);
+          if (RC_PROF > 1) {
+            hz[0] += clock64() - th0;
+            hz[1] += (rc_uniform(L.seg[H + 1]) - kf + 63) / 64;
+          }
         }
       }
+      if (RC_PROF == 3) __syncthreads();  // the head walked alone (profiling only)
       const bool sit_out = RC_HEAD_SIMD == 1 && H != RC_NONE && wv != 0 && (wv & 3u) == 0;
       for (; !sit_out;) {
         const uint32_t j = rc_uniform(atomicAdd(&L.qlong, 1u)) >> 6;
@@ -544,8 +565,8 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
           const uint64_t dt = clock64() - tb0;
           busy += dt;
           if (j < nhuge) {
-            hz[it == 0 ? 0 : 2] += dt;
-            hz[it == 0 ? 1 : 3] += (rc_uniform(L.seg[sg + 1]) - kf + 63) / 64;
+            hz[2] += dt;
+            hz[3] += (rc_uniform(L.seg[sg + 1]) - kf + 63) / 64;
           }
         }
       }
@@ -625,6 +646,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
     g->dbg[0] += iters;
     if (RC_PROF == 1)
       for (int k = 0; k < 4; k++) g->dbg[2 + k] += prof[k];
+    if (RC_PROF > 1) g->dbg[3] += prof[1];  // the walk phase
     g->res_chunk_windows++;
   }
 }
