@@ -231,13 +231,22 @@ struct Walker {
   __device__ __attribute__((always_inline)) uint32_t transfer(const WPre& e) {
     const uint32_t i = e.i;
     if (e.cls & C_STATIC) return e.code;
+    // The key-map reads whose entries are known now (this event's id, a post/void's pending id) go
+    // out with the event body's load: a component's walk is a chain of dependent reads, and nothing
+    // this event does before their original use writes them.
+    const bool pv = e.cls & C_POSTVOID;
+    const int32_t c = e.id_alone ? -1 : bmap_committed(s.bmap, e.id_ent, epoch);
+    int32_t pc = -1;
+    if (pv && e.p_tslot == NONE32) {
+      pc = pcache_find(e.pid_ent);
+      if (pc < 0) pc = bmap_committed(s.bmap, e.pid_ent, epoch);
+    }
     tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev)[i];
     t.id.lo = ((uint64_t)e.head.y << 32) | e.head.x;
     t.id.hi = ((uint64_t)e.head.w << 32) | e.head.z;
     t.timestamp = win_ts(*w, e.b, i);
-    if (e.cls & C_POSTVOID) return post_or_void(e, t);
+    if (pv) return post_or_void(e, t, c, pc);
     if (e.id_tslot != NONE32) return ct_exists(t, d.xr[e.id_tslot]);
-    const int32_t c = e.id_alone ? -1 : bmap_committed(s.bmap, e.id_ent, epoch);
     if (c >= 0) return ct_exists(t, s.t2[c]);
     const uint32_t drs = e.dr, crs = e.cr;
     tb_account_t* dra = &d.acc[drs];
@@ -282,33 +291,35 @@ struct Walker {
     return TB_CT_OK;
   }
 
-  // post_or_void_pending_transfer (:1608-1741) from the pending lookup on.
-  __device__ __attribute__((always_inline)) uint32_t post_or_void(const WPre& e, const tb_transfer_t& t) {
+  // post_or_void_pending_transfer (:1608-1741) from the pending lookup on. `c`: this event's id
+  // committed earlier in the window (or -1); `pc`: the in-window pending transfer (-1: none, or the
+  // pending transfer was stored before the window: p_tslot). The pending record, its accounts and its
+  // status are read together.
+  __device__ __attribute__((always_inline)) uint32_t post_or_void(const WPre& e, const tb_transfer_t& t, int32_t c,
+                                                                  int32_t pc) {
     const uint32_t i = e.i;
     const uint32_t pslot = e.p_tslot;
-    int32_t pc = -1;
     uint32_t drs, crs;
+    uint8_t pst0;
     const tb_transfer_t* pp;  // one load from the selected record (no merged aggregate)
     if (pslot != NONE32) {
       pp = &d.xr[pslot];
       drs = e.dr;
       crs = e.cr;
+      pst0 = d.xstatus[pslot];
     } else {
-      pc = pcache_find(e.pid_ent);
-      if (pc < 0) pc = bmap_committed(s.bmap, e.pid_ent, epoch);
       if (pc < 0) return TB_CT_PENDING_TRANSFER_NOT_FOUND;
       pp = &s.t2[pc];
       drs = s.dr_slot[pc];
       crs = s.cr_slot[pc];
+      pst0 = s.bstatus[pc];
     }
     const tb_transfer_t p = *pp;
     u128 amount;
     uint32_t r = pv_against(t, p, &amount);
     if (r != CONT) return r;
     if (e.id_tslot != NONE32) return pv_exists(t, d.xr[e.id_tslot], p);
-    const int32_t c = e.id_alone ? -1 : bmap_committed(s.bmap, e.id_ent, epoch);
     if (c >= 0) return pv_exists(t, s.t2[c], p);
-    const uint8_t pst0 = pc >= 0 ? s.bstatus[pc] : d.xstatus[pslot];
     uint8_t pst = pst0;
     if (pst == TB_PENDING_PENDING && xw_expired_before(*w, p, s.batch[i])) pst = TB_PENDING_EXPIRED;
     r = pv_status(pst);
