@@ -72,7 +72,7 @@ PHASE_KERNELS = {
     "cpw": ["k_cc_walk<true>", "k_cc_init", "k_cc_link", "k_cc_keys", "onesweep sort", "k_cc_segs"],
     "classify": ["k_classify<true>"], "wlist": ["k_wlist"], "walk": ["k_walk<true>", "k_wfold"],
     "pulse": ["k_pulse", "k_xwin_rb", "k_xwin_minlive", "k_xwin_replay", "k_xwin_expire"],
-    "fused": ["k_ct_fused", "k_fu_final"],
+    "fused": ["k_ct_fused"],  # k_fu_final (replies, ~12 us per 1M) runs outside the timed phase
 }
 # the walkers (cpw, walk) run the reference loop for the events they decide: event 128, balance
 # pairs 2 x 32, record 128 per walked event
