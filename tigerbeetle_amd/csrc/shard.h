@@ -272,6 +272,8 @@ __global__ void __launch_bounds__(SEG) k_sh_roles(Dev d, Scratch s, const uint8_
   __shared__ uint32_t aux;
   const uint32_t i = blockIdx.x * SEG + threadIdx.x;
   if (threadIdx.x == 0) aux = 0;
+  // exchange 1's trailer (written by later kernels of the window only): zeroed here, not by a memset
+  if (i < 4) xch.trailer[i] = 0;
   __syncthreads();
   uint32_t roles = 0;
   if (i < E) {
@@ -460,7 +462,11 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ca(Dev d, Scratch s, const tb_
 // ------------------------------------------------------------------------------------------------
 template <bool XFER>
 __global__ void __launch_bounds__(256) k_sh_home(Scratch s, const uint8_t* __restrict__ ev_bytes, WinDesc w,
-                                                 uint32_t e0, uint32_t e1, uint32_t* trailer2) {
+                                                 uint32_t e0, uint32_t e1, uint32_t* trailer2,
+                                                 unsigned long long* bits, uint32_t nwords) {
+  // every commit-bit word of the window starts at zero (k_sh_reply writes this home's words; the
+  // all-reduce sums every shard's): zeroed here rather than by a memset launch
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nwords; k += gridDim.x * blockDim.x) bits[k] = 0;
   const uint32_t i = e0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= e1) return;
   const uint32_t b = win_batch(w, i);
