@@ -4,7 +4,8 @@ restatement batch by batch under the harness protocol. Replies per batch, then t
 byte and through the whole-state digest (tbg_digest vs tigerbeetle_amd.digest over the oracle's
 dumps).
 
-- cfg2: uniform transfers, device-generated exactly as bench.py generates them;
+- cfg2: uniform transfers, device-generated exactly as bench.py generates them, window by window
+  and queued without syncs (fused-only windows, the bench's timed path);
 - cfg4 mixed at window scale: two-phase, posts/voids, chains with injected failures in 1M-event
   windows (no tick inside a window: the component walkers and the pulse_next replay at scale);
 - cfg4 as bench.py runs it: +1 s per batch, 128-batch windows with ~127 pulses inside each;
@@ -88,6 +89,55 @@ def test_geometry_cfg2_uniform(id_order):
         st = gpu.stats()
         assert st["transfers"] == n_x
         assert (st["sorted_transfers"] == n_x) == (id_order == "sequential")
+        # rising ids: every window is order-free and committed by the fused pass (fused.h)
+        assert (st["fused_windows"] == n_win) == (id_order == "sequential")
+        _check_digest(gpu, ref)
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_geometry_cfg2_queued_fused_only_windows():
+    """bench.py's timed cfg2 path exactly: 128-batch windows queued back to back with no sync in
+    between (each launched fused-only: pulse + k_ct_fused + k_fu_final), each with its own reply
+    buffers, then one tbg_sync; every window's replies, the stores and the digest vs the restatement."""
+    import torch
+
+    from tigerbeetle_amd import StateMachine, _lib
+
+    L = _lib.lib()
+    n_win, seed = 3, 45
+    n_x = n_win * 128 * BM
+    gpu = StateMachine(batch_max=BM, accounts_max=N_ACC, transfers_max=n_x, window_events_max=128 * BM)
+    ref = OracleStateMachine(batch_max=BM)
+    try:
+        _accounts(gpu, ref, seed)
+        d_x = torch.empty(n_x * 128, dtype=torch.uint8, device="cuda")
+        outs = [(torch.zeros(128 * BM * 8, dtype=torch.uint8, device="cuda"),
+                 torch.zeros(129, dtype=torch.int32, device="cuda")) for _ in range(n_win)]
+        torch.cuda.synchronize()
+        _lib.check(L.tbg_gen_transfers_uniform(d_x.data_ptr(), 0, n_x, seed, N_ACC, 0, gpu.stream), "gen")
+        gpu.sync()
+        host = workload.transfers_uniform(0, n_x, seed, N_ACC)
+        for w in range(n_win):
+            ns, ts = [], []
+            for _ in range(128):
+                gpu.prepare_timestamp += 1 + BM
+                ns.append(BM)
+                ts.append(gpu.prepare_timestamp)
+            d_res, d_base = outs[w]
+            gpu.commit_window(Operation.create_transfers, d_x.data_ptr() + w * 128 * BM * 128, ns, ts,
+                              d_res.data_ptr(), d_base.data_ptr(), True, ts[0])
+        gpu.sync()
+        for w in range(n_win):
+            d_res, d_base = outs[w]
+            base, res = to_host(d_base), to_host(d_res).tobytes()
+            r = oracle_batches(ref, Operation.create_transfers, _batches(host, w * 128 * BM, 128 * BM))
+            assert [res[base[b] * 8: base[b + 1] * 8] for b in range(128)] == r
+        st = gpu.stats()
+        assert st["transfers"] == n_x and st["fused_windows"] == n_win
         _check_digest(gpu, ref)
         _compare_final(gpu, ref)
     finally:
