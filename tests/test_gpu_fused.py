@@ -252,3 +252,69 @@ def test_fused_only_windows_replayed_at_sync(bad_windows):
     finally:
         gpu.close()
         ref.close()
+
+
+@pytest.mark.gpu
+def test_fused_only_pulse_skip_until_pending_timeouts():
+    """Fused-only windows skip their pulse launch while pulse_next is "never" (host.inc
+    launch_window). Queued without syncs: simple windows, then one that creates pending transfers
+    with a 1 s timeout (it leaves the class: replayed at sync), then, 2 s later, windows whose harness
+    pulse expires them. Every window's replies, pulse_next and the stores equal the restatement's."""
+    import torch
+
+    from tigerbeetle_amd.state_machine import to_host
+    from tigerbeetle_amd.types import NS_PER_S
+    from test_gpu_window import oracle_batches as ob
+
+    n_acc = 2000
+    gpu, ref = _engines(n_acc, 1 << 19)
+    try:
+        _accounts(gpu, ref, n_acc)
+        first = 0
+
+        def submit(batches, tick):
+            nonlocal first
+            gpu.prepare_timestamp += tick
+            ns, ts = [], []
+            for ev in batches:
+                gpu.prepare_timestamp += 1 + len(ev)
+                ns.append(len(ev))
+                ts.append(gpu.prepare_timestamp)
+            data = np.concatenate([np.frombuffer(ev.tobytes(), np.uint8) for ev in batches])
+            d_ev = torch.from_numpy(data.copy()).cuda()
+            d_res = torch.zeros(sum(ns) * 8, dtype=torch.uint8).cuda()
+            d_base = torch.zeros(len(ns) + 1, dtype=torch.int32).cuda()
+            torch.cuda.synchronize()
+            gpu.commit_window(Operation.create_transfers, d_ev.data_ptr(), ns, ts, d_res.data_ptr(),
+                              d_base.data_ptr(), True, ts[0])
+            return (d_ev, d_res, d_base, len(ns)), ob(ref, Operation.create_transfers, batches, tick)
+
+        def check(outs):
+            for (d_ev, d_res, d_base, nb), r in outs:
+                res, base = to_host(d_res).tobytes(), to_host(d_base)
+                assert [res[base[b] * 8: base[b + 1] * 8] for b in range(nb)] == r
+
+        outs = []
+        for w in range(2):  # before the first settle: pulses launched
+            outs.append(submit(_window(first, n_acc), 0))
+            first += WIN * BM
+        gpu.sync()  # settle: pulse_next is never from here
+        check(outs)
+        outs = [submit(_window(first, n_acc), 0)]
+        first += WIN * BM
+        pend = _window(first, n_acc)
+        first += WIN * BM
+        for ev in pend[2:5]:
+            ev["flags"][::50] = 2   # pending
+            ev["timeout"][::50] = 1  # expires 1 s after its timestamp
+        outs.append(submit(pend, 0))
+        for tick in (2 * NS_PER_S, 0, NS_PER_S):  # pulses due from here
+            outs.append(submit(_window(first, n_acc), tick))
+            first += WIN * BM
+        gpu.sync()
+        check(outs)
+        assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
