@@ -147,6 +147,7 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t fu_windows;  // cumulative windows committed by the fused pass
   uint32_t fu_fail_epoch;  // the fused-only window that left the class (window_error bit 3)
   uint32_t sh_mis;         // sharded: this shard's ledger-mismatch slots used this window (shard.h)
+  uint32_t sh_unsup;       // sharded: a home event outside the class this window (k_sh_count -> trailer 2)
 };
 
 // The fused pass (fused.h) committed this window: the general path's kernels return at once.

@@ -272,8 +272,10 @@ __global__ void __launch_bounds__(SEG) k_sh_roles(Dev d, Scratch s, const uint8_
   __shared__ uint32_t aux;
   const uint32_t i = blockIdx.x * SEG + threadIdx.x;
   if (threadIdx.x == 0) aux = 0;
-  // exchange 1's trailer (written by later kernels of the window only): zeroed here, not by a memset
+  // exchange 1's trailer (written by later kernels of the window only): zeroed here, not by a memset;
+  // so is the homes' out-of-class flag that k_sh_count turns into exchange 2's trailer
   if (i < 4) xch.trailer[i] = 0;
+  if (i == 0) d.g->sh_unsup = 0;
   __syncthreads();
   uint32_t roles = 0;
   if (i < E) {
@@ -551,8 +553,12 @@ __global__ void __launch_bounds__(256) k_sh_decide(Scratch s, const uint8_t* ev,
 }
 
 // Home slice, per segment k0 + blockIdx.x (segments are window-aligned, SEG events): failure counts.
-__global__ void __launch_bounds__(SEG) k_sh_count(Scratch s, uint32_t e0, uint32_t e1, uint32_t k0) {
+__global__ void __launch_bounds__(SEG) k_sh_count(Scratch s, uint32_t e0, uint32_t e1, uint32_t k0,
+                                                  const uint32_t* unsup, uint32_t* trailer2) {
   __shared__ uint32_t lds[SEG / 64];
+  // exchange 2's trailer from the homes' flag (k_sh_home / k_sh_decide, earlier launches): written
+  // whole here instead of a memset before them
+  if (blockIdx.x == 0 && threadIdx.x < 4) trailer2[threadIdx.x] = threadIdx.x == 0 ? *unsup : 0u;
   const uint32_t i = (k0 + blockIdx.x) * SEG + threadIdx.x;
   const uint32_t nbad = (i >= e0 && i < e1 && s.code[i] != TB_CT_OK) ? 1u : 0u;
   const uint32_t tot = block_sum<SEG / 64>(nbad, lds);
