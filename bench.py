@@ -149,10 +149,16 @@ def parse():
                    help="cfg1/cfg2: after the timed run, commit this many further transfers of the same stream "
                         "from pinned host memory (tbg_commit_window_host, H2D overlapped with compute) and report "
                         "it as `host_fed` (never `value`); default 32 windows (the pipeline fill, one unoverlapped H2D, is 1/32 of it), 0 = off")
-    p.add_argument("--id-order", default="sequential", choices=["sequential", "random", "reversed"],
+    p.add_argument("--id-order", default="sequential", choices=["sequential", "random", "reversed", "time"],
                    help="account and transfer ids as the reference benchmark's --id-order (cli.zig:97, 263-265; "
                         "testing/id.zig IdPermutation; random = pseudo-UUIDs from Xoshiro256, the reference's own ids "
-                        "for the permutation seed DefaultPrng(seed) draws first)")
+                        "for the permutation seed DefaultPrng(seed) draws first); time = the time-based 128-bit ids "
+                        "the reference's docs recommend (docs/develop/data-modeling.md:186-203: 48-bit ms above 80 "
+                        "random bits, strictly increasing)")
+    p.add_argument("--sync-commit-batches", type=int, default=None,
+                   help="cfg1/cfg2: after the timed run, commit this many further batches one at a time through the "
+                        "synchronous tbg_prefetch + tbg_commit from host memory (a replica that does not pipeline) and "
+                        "report it as `sync_commit` (never `value`); default 64, 0 = off")
     p.add_argument("--change-log", action="store_true",
                    help="engine keeps the write-back change log (TBG_FLAG_CHANGE_LOG): its device cost")
     a = p.parse_args()
@@ -167,6 +173,8 @@ def parse():
         a.warmup = 256 if a.config == "cfg2" else 32
     if a.host_fed_transfers is None:
         a.host_fed_transfers = 32 * min(a.window, WINDOW_BATCHES_MAX) * BATCH if a.config in ("cfg1", "cfg2") else 0
+    if a.sync_commit_batches is None:
+        a.sync_commit_batches = 64 if a.config in ("cfg1", "cfg2") else 0
     a.tick = c["tick"]
     from tigerbeetle_amd import workload
 
@@ -275,10 +283,56 @@ def host_fed(args, sm, torch, first, n_acc, seed, win):
                     "overlapping the previous window's kernels) -> replies D2H to pinned host memory"}
 
 
+def sync_commit(args, sm, first, n_acc, seed):
+    """The replica that does not pipeline: `k` further batches of the same stream, each through the
+    synchronous StateMachine calls of the reference protocol (state_machine.zig:2719-2739: pulse()
+    check, prefetch, commit), request bytes in pageable host memory, replies copied back per batch
+    (include/tbg.h tbg_prefetch / tbg_commit). Timed from the first call to the last reply."""
+    from tigerbeetle_amd import workload
+    from tigerbeetle_amd.types import Operation
+
+    k = args.sync_commit_batches
+    evs = workload.permute_ids(workload.transfers_uniform(first, k * BATCH, seed, n_acc), args.id_order_code,
+                               args.perm_seed)
+    bodies = [evs[b * BATCH:(b + 1) * BATCH].tobytes() for b in range(k)]
+    fails = 0
+    t0 = time.perf_counter()
+    for b, body in enumerate(bodies):
+        sm.prepare_timestamp += 1 + BATCH
+        T = sm.prepare_timestamp
+        if sm.pulse():
+            sm.commit(0, 2 * b, T, Operation.pulse, b"")
+        sm.prefetch_timestamp = T
+        sm.prefetch(2 * b + 1, Operation.create_transfers, body)
+        fails += len(sm.commit(0, 2 * b + 1, T, Operation.create_transfers, body)) // 8
+    wall = time.perf_counter() - t0
+    return {"value": round(k * BATCH / wall, 1), "unit": "transfers/s", "batches": k, "transfers": k * BATCH,
+            "failed_events": fails, "us_per_batch": round(wall / k * 1e6, 1),
+            "path": "per batch: pulse() check, tbg_prefetch (H2D of the 1 MiB request), tbg_commit (device "
+                    "commit, reply D2H, synchronous) - the reference StateMachine call sequence"}
+
+
 def cpu_baseline(args, seed):
     """Single-threaded C restatement (oracle/liboracle.so) on a time-bounded prefix of the same
     stream, same harness protocol (pulse when due, then the batch); only the commit calls are
-    timed. Setup (accounts, cfg3 funding) is untimed, as on the GPU."""
+    timed. Setup (accounts, cfg3 funding) is untimed, as on the GPU. The process is
+    pinned to one host core for the measurement (restored after)."""
+    try:
+        saved = os.sched_getaffinity(0)
+        pinned = min(saved)
+        os.sched_setaffinity(0, {pinned})
+    except (AttributeError, OSError):
+        saved, pinned = None, None
+    try:
+        line = _cpu_baseline(args, seed)
+    finally:
+        if saved is not None:
+            os.sched_setaffinity(0, saved)
+    line["pinned_cpu"] = pinned
+    return line
+
+
+def _cpu_baseline(args, seed):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_sm import lib as olib
 
@@ -321,7 +375,7 @@ def cpu_baseline(args, seed):
         "cores": 1,
         "kind": "port",
         "sample": f"first {events} transfers of the same {args.config} stream (same accounts and setup), "
-                  f"{spent:.1f} s of commit time on 1 host core (oracle/tb_oracle.c, -O2)",
+                  f"{spent:.1f} s of commit time on 1 pinned host core (oracle/tb_oracle.c, -O2 -march=x86-64-v2)",
     }
     line.update(host_cpu())
     return line
@@ -578,7 +632,7 @@ def main():
     seed = args.seed + 1000 * rank  # independent stream per shard
 
     sm = StateMachine(device=device, batch_max=BATCH, accounts_max=n_acc_total,
-                      transfers_max=n_xfer + n_setup + args.host_fed_transfers,
+                      transfers_max=n_xfer + n_setup + args.host_fed_transfers + args.sync_commit_batches * BATCH,
                       window_events_max=win * BATCH,
                       resolver={"chunks": True, "relax": "relax", "wait": "wait", "off": False}[args.resolver],
                       change_log=args.change_log)
@@ -770,6 +824,11 @@ def main():
         if args.host_fed_transfers and cfg in ("cfg1", "cfg2") and world == 1:
             sm.prepare_timestamp = prepare_ts
             line["host_fed"] = host_fed(args, sm, torch, n_xfer, n_acc, seed, win)
+            prepare_ts = sm.prepare_timestamp
+        if args.sync_commit_batches and cfg in ("cfg1", "cfg2") and world == 1:
+            sm.prepare_timestamp = prepare_ts
+            line["sync_commit"] = sync_commit(args, sm, n_xfer + args.host_fed_transfers // BATCH * BATCH, n_acc,
+                                              seed)
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, seed)
         print(json.dumps(line), flush=True)

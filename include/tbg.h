@@ -344,6 +344,7 @@ typedef struct tbg_stats {
     uint64_t sorted_transfers; /* leading transfer records in the sorted id prefix (not hashed) */
     uint64_t chunked_windows;  /* balance-limit windows the chunked resolver decided */
     uint64_t fused_windows;    /* order-free transfer windows committed in one pass (fused.h) */
+    uint64_t ovf_rescans;     /* times the overflow bound was re-tightened (restore.h k_ovf_rescan) */
 } tbg_stats;
 int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
 

@@ -318,3 +318,169 @@ def test_fused_only_pulse_skip_until_pending_timeouts():
     finally:
         gpu.close()
         ref.close()
+
+
+def _queue(gpu, batches, tick=0, op=Operation.create_transfers):
+    """One device-resident window (tbg_commit_window, harness pulse), no sync."""
+    import torch
+
+    gpu.prepare_timestamp += tick
+    ns, ts = [], []
+    for ev in batches:
+        gpu.prepare_timestamp += 1 + len(ev)
+        ns.append(len(ev))
+        ts.append(gpu.prepare_timestamp)
+    data = np.concatenate([np.frombuffer(ev.tobytes(), np.uint8) for ev in batches])
+    d_ev = torch.from_numpy(data.copy()).cuda()
+    d_res = torch.zeros(max(sum(ns), 1) * 8, dtype=torch.uint8).cuda()
+    d_base = torch.zeros(len(ns) + 1, dtype=torch.int32).cuda()
+    torch.cuda.synchronize()
+    gpu.commit_window(op, d_ev.data_ptr(), ns, ts, d_res.data_ptr(), d_base.data_ptr(), True, ts[0])
+    return d_ev, d_res, d_base, len(ns)
+
+
+def _replies(handle):
+    from tigerbeetle_amd.state_machine import to_host
+
+    _, d_res, d_base, nb = handle
+    res, base = to_host(d_res).tobytes(), to_host(d_base)
+    return [res[base[b] * 8: base[b + 1] * 8] for b in range(nb)]
+
+
+@pytest.mark.gpu
+def test_fused_backoff_from_device_commit_then_fused_only_windows():
+    """A tbg_commit_device batch outside the class (its fused attempt backs the speculation off, and
+    no settle follows) and then device-resident windows queued without syncs: the first of them
+    finds the back-off in k_ct_fused and must hand itself to settle()'s replay instead of being
+    dropped (the window was silently never committed)."""
+    import torch
+
+    from tigerbeetle_amd.state_machine import to_host
+
+    n_acc = 2000
+    gpu, ref = _engines(n_acc, 1 << 19)
+    try:
+        _accounts(gpu, ref, n_acc)
+        first = 0
+        _check(gpu, ref, _window(first, n_acc))
+        first += WIN * BM
+        gpu.sync()
+        # one batch through tbg_commit_device, outside the class (a pending transfer)
+        ev = workload.transfers_uniform(first, BM, seed=17, n_accounts=n_acc)
+        first += BM
+        ev["flags"][10] = 2
+        gpu.prepare_timestamp += 1 + BM
+        T = gpu.prepare_timestamp
+        d_ev = torch.from_numpy(np.frombuffer(ev.tobytes(), np.uint8).copy()).cuda()
+        d_res = torch.zeros(BM * 8, dtype=torch.uint8).cuda()
+        d_cnt = torch.zeros(1, dtype=torch.int32).cuda()
+        torch.cuda.synchronize()
+        gpu.commit_device(Operation.create_transfers, T, d_ev.data_ptr(), BM, d_res.data_ptr(), d_cnt.data_ptr(),
+                          True, T)
+        want0 = oracle_batches(ref, Operation.create_transfers, [ev])[0]
+        outs, expect = [], []
+        for w in range(4):
+            batches = _window(first, n_acc, seed=18)
+            first += WIN * BM
+            outs.append(_queue(gpu, batches))
+            expect.append(oracle_batches(ref, Operation.create_transfers, batches))
+        gpu.sync()
+        c = int(to_host(d_cnt)[0])
+        assert to_host(d_res).tobytes()[:c * 8] == want0
+        for h, r in zip(outs, expect):
+            assert _replies(h) == r
+        assert gpu.stats()["transfers"] == len(ref.dump_transfers())
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_sync_pending_commit_then_fused_only_windows_pulse():
+    """After a settle found pulse_next "never", a synchronous tbg_commit (prefetch + commit) creates
+    pending transfers with a 1 s timeout; fused-only windows queued 2 s later must launch their pulse
+    and expire them (the general path left pn_never set, so the expiries were skipped)."""
+    from chaos import run_protocol
+
+    from tigerbeetle_amd.types import NS_PER_S
+
+    n_acc = 2000
+    gpu, ref = _engines(n_acc, 1 << 19)
+    try:
+        _accounts(gpu, ref, n_acc)
+        first = 0
+        for w in range(2):
+            _check(gpu, ref, _window(first, n_acc))
+            first += WIN * BM
+        gpu.sync()  # pulse_next is never here
+        ev = workload.transfers_uniform(first, 64, seed=19, n_accounts=n_acc)
+        first += 64
+        ev["flags"][::4] = 2
+        ev["timeout"][::4] = 1
+        assert run_protocol(gpu, Operation.create_transfers, ev) == run_protocol(ref, Operation.create_transfers, ev)
+        outs, expect = [], []
+        for w, tick in enumerate((2 * NS_PER_S, 0)):
+            batches = _window(first, n_acc, seed=20)
+            first += WIN * BM
+            outs.append(_queue(gpu, batches, tick))
+            expect.append(oracle_batches(ref, Operation.create_transfers, batches, tick))
+        gpu.sync()
+        for h, r in zip(outs, expect):
+            assert _replies(h) == r
+        assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
+        st = gpu.dump_transfer_status()
+        assert (st == 4).sum() == 16  # every pending transfer expired
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_fused_resumes_after_overflow_bound_passes_2_63():
+    """Globals::ovf_bound sums every committed amount (it must bound every dp+dpo / cp+cpo without
+    reading them). Amounts just below the fused class's 2^43 cap, queued without syncs, drive it past
+    2^63 (~128 windows of 8192 events), where the fused pass stops (windows replayed through the
+    general path at sync). The next state read re-tightens it to the accounts' largest balance sum
+    (restore.h k_ovf_rescan, ~2^53 here), and the fused pass resumes. Replies and stores vs the
+    restatement throughout."""
+    n_acc = 2000
+    gpu, ref = _engines(n_acc, 1 << 21)
+    try:
+        _accounts(gpu, ref, n_acc)
+        first, outs = 0, []
+        big = (1 << 43) - 1
+
+        def win():
+            nonlocal first
+            b = _window(first, n_acc, seed=23)
+            first += WIN * BM
+            for ev in b:
+                ev["amount_lo"] = big - (ev["amount_lo"] % 4096)
+            return b
+
+        for w in range(132):
+            b = win()
+            outs.append((_queue(gpu, b), oracle_batches(ref, Operation.create_transfers, b)))
+        gpu.sync()
+        st0 = gpu.stats()
+        assert st0["fused_windows"] < 132  # the bound passed 2^63 inside the queue
+        for h, r in outs:
+            assert _replies(h) == r
+        assert st0["ovf_rescans"] == 0
+        outs = []
+        for w in range(6):
+            b = win()
+            h = _queue(gpu, b)
+            gpu.sync()
+            outs.append((h, oracle_batches(ref, Operation.create_transfers, b)))
+        for h, r in outs:
+            assert _replies(h) == r
+        st1 = gpu.stats()
+        assert st1["ovf_rescans"] >= 1
+        assert st1["fused_windows"] >= st0["fused_windows"] + 3  # back on the fused pass
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()

@@ -47,12 +47,13 @@ def _accounts(gpu, ref, seed, order=0, perm_seed=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("id_order", ["sequential", "random", "reversed"])
+@pytest.mark.parametrize("id_order", ["sequential", "random", "reversed", "time"])
 def test_geometry_cfg2_uniform(id_order):
     """bench.py's cfg2 path: device-generated stream, tbg_commit_window over 128 batches; with
     `bench.py --id-order` random / reversed (the reference benchmark's IdPermutation, cli.zig:263-265)
     every account and transfer id is permuted, so the windows take the hashed id path (no sorted
-    prefix, key-map claims)."""
+    prefix, key-map claims); time = the recommended time-based 128-bit ids (strictly increasing, high
+    word nonzero): fused pass and sorted prefix in u128 order."""
     import torch
 
     from tigerbeetle_amd import StateMachine, _lib
@@ -88,11 +89,77 @@ def test_geometry_cfg2_uniform(id_order):
             assert [res[base[b] * 8: base[b + 1] * 8] for b in range(128)] == r
         st = gpu.stats()
         assert st["transfers"] == n_x
-        assert (st["sorted_transfers"] == n_x) == (id_order == "sequential")
+        rising = id_order in ("sequential", "time")
+        assert (st["sorted_transfers"] == n_x) == rising
         # rising ids: every window is order-free and committed by the fused pass (fused.h)
-        assert (st["fused_windows"] == n_win) == (id_order == "sequential")
+        assert (st["fused_windows"] == n_win) == rising
+        if id_order == "time":  # lookups through the u128 sorted prefix: every id, one absent
+            q = np.zeros(BM, [("lo", "<u8"), ("hi", "<u8")])
+            pick = np.linspace(0, n_x - 1, BM - 1).astype(np.int64)
+            q["lo"][:-1], q["hi"][:-1] = host["id_lo"][pick], host["id_hi"][pick]
+            q["lo"][-1], q["hi"][-1] = host["id_lo"][5] + 1, host["id_hi"][5]
+            assert gpu.commit(0, 1, 0, Operation.lookup_transfers, q.tobytes()) == \
+                ref.commit(0, 1, 0, Operation.lookup_transfers, q.tobytes())
         _check_digest(gpu, ref)
         _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("id_order", ["sequential", "time"])
+def test_geometry_cfg2_change_log(id_order):
+    """The drop-in configuration (TBG_FLAG_CHANGE_LOG, write-back to the forest) at the
+    bench's geometry: windows committed by the fused pass with the change log on; after each window
+    the logged transfers are the window's records and the logged accounts exactly the accounts it
+    changed, each equal to the restatement's record."""
+    import torch
+
+    from test_gpu_changes import _by_id
+    from tigerbeetle_amd import StateMachine, _lib
+
+    L = _lib.lib()
+    n_win, seed = 2, 46
+    order = workload.ID_ORDERS[id_order]
+    perm_seed = workload.benchmark_permutation_seed(seed)
+    n_x = n_win * 128 * BM
+    gpu = StateMachine(batch_max=BM, accounts_max=N_ACC, transfers_max=n_x, window_events_max=128 * BM,
+                       change_log=True)
+    ref = OracleStateMachine(batch_max=BM)
+    try:
+        _accounts(gpu, ref, seed, order, perm_seed)
+        d_x = torch.empty(n_x * 128, dtype=torch.uint8, device="cuda")
+        d_res = torch.zeros(128 * BM * 8, dtype=torch.uint8, device="cuda")
+        d_base = torch.zeros(129, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        _lib.check(L.tbg_gen_transfers_uniform(d_x.data_ptr(), 0, n_x, seed, N_ACC, 0, gpu.stream), "gen")
+        _lib.check(L.tbg_gen_permute_ids(d_x.data_ptr(), n_x, 1, order, perm_seed, gpu.stream), "permute")
+        host = workload.permute_ids(workload.transfers_uniform(0, n_x, seed, N_ACC), order, perm_seed)
+        for w in range(n_win):
+            acc0, nx0 = ref.dump_accounts(), len(ref.dump_transfers())
+            ns, ts = [], []
+            for _ in range(128):
+                gpu.prepare_timestamp += 1 + BM
+                ns.append(BM)
+                ts.append(gpu.prepare_timestamp)
+            gpu.commit_window(Operation.create_transfers, d_x.data_ptr() + w * 128 * BM * 128, ns, ts,
+                              d_res.data_ptr(), d_base.data_ptr(), True, ts[0])
+            gpu.sync()
+            base = to_host(d_base)
+            res = to_host(d_res).tobytes()
+            r = oracle_batches(ref, Operation.create_transfers, _batches(host, w * 128 * BM, 128 * BM))
+            assert [res[base[b] * 8: base[b + 1] * 8] for b in range(128)] == r
+            acc1, x1 = ref.dump_accounts(), ref.dump_transfers()
+            la, lx, rows = gpu.window_changes()
+            assert lx.tobytes() == x1[nx0:].tobytes()
+            after, before, logged = _by_id(acc1), _by_id(acc0), _by_id(la)
+            changed = {k for k, v in after.items() if before.get(k) != v}
+            assert set(logged) == changed and len(logged) == len(la)
+            assert all(after[k] == v for k, v in logged.items())
+            assert len(rows) == 0
+        assert gpu.stats()["fused_windows"] == n_win
+        _check_digest(gpu, ref)
     finally:
         gpu.close()
         ref.close()

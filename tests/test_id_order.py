@@ -55,7 +55,7 @@ def test_permute_records_cpu():
     a = workload.accounts(0, 100, seed=3)
     t = workload.transfers_uniform(0, 100, seed=3, n_accounts=100)
     seed = workload.benchmark_permutation_seed(3)
-    for order in (1, 2):
+    for order in (1, 2, 3):
         a2 = workload.permute_ids(a.copy(), order, seed)
         t2 = workload.permute_ids(t.copy(), order, seed)
         ids = {(int(x), int(y)) for x, y in zip(a2["id_lo"], a2["id_hi"])}
@@ -65,8 +65,22 @@ def test_permute_records_cpu():
         assert (t2["id_hi"] != 0).all()
 
 
+def test_time_ids_strictly_increasing():
+    """The time-based order (docs/develop/data-modeling.md:186-203): 48-bit milliseconds above 80
+    random bits, incremented within a millisecond; strictly increasing u128 ids, high word nonzero,
+    a new millisecond every 2^18 ids."""
+    n = (1 << 18) * 3 + 1000
+    lo, hi = workload.encode_ids(np.arange(1, n + 1, dtype=np.uint64), 3, 77)
+    v = [int(a) | (int(b) << 64) for a, b in zip(lo, hi)]
+    assert all(x < y for x, y in zip(v, v[1:]))
+    assert (hi != 0).all()
+    ms = [x >> 80 for x in v]
+    assert ms[0] == workload.TIME_BASE_MS and ms[-1] == workload.TIME_BASE_MS + 3
+    assert ms[(1 << 18) - 1] == ms[0] and ms[1 << 18] == ms[0] + 1
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("order", [1, 2, 3])
 def test_permute_ids_device(order):
     import torch
 

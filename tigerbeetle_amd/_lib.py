@@ -56,7 +56,7 @@ class Stats(ctypes.Structure):
                 ("events_total", ctypes.c_uint64), ("walker_events", ctypes.c_uint64),
                 ("resolver_events", ctypes.c_uint64), ("component_events", ctypes.c_uint64),
                 ("sorted_transfers", ctypes.c_uint64), ("chunked_windows", ctypes.c_uint64),
-                ("fused_windows", ctypes.c_uint64)]
+                ("fused_windows", ctypes.c_uint64), ("ovf_rescans", ctypes.c_uint64)]
 
 
 class Demuxer(ctypes.Structure):

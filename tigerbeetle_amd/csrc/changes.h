@@ -7,7 +7,10 @@
 //   - inserted records are the store slice [base, count) of the window (commit = timestamp order);
 //   - every account whose balances a committed event changed is marked with the window number
 //     (k_chg_mark; plain stores, every writer stores the same value), then listed in slot order
-//     (k_chg_count, k_chg_scan, k_chg_list);
+//     (k_chg_count, k_chg_scan, k_chg_list). The fused pass (fused.h) marks its accounts in `fmark`
+//     while it applies, before it knows whether it commits the window: those marks count only when
+//     it did (Globals::sp_done with fu_epoch = the window), and the general path's own marks in
+//     `mark` otherwise;
 //   - earlier pending transfers that a committed post/void resolved are listed by k_chg_mark.
 // k_pulse_tail marks the accounts and lists the transfers of every expiry the same way. A commit
 // call's log covers its pulse (if any) and its window. tbg_window_changes gathers and copies them.
@@ -16,6 +19,7 @@
 
 struct ChgLog {
   uint32_t* mark;      // per account slot: window number of the last change
+  uint32_t* fmark;     // per account slot: window number of the last fused-pass change (speculative)
   uint32_t* list;      // changed account slots, ascending
   uint32_t* pend;      // transfer slots of earlier pending transfers resolved in the window
   uint32_t* seg;       // per account segment: count, then exclusive offset
@@ -27,7 +31,8 @@ struct ChgLog {
 template <bool XFER>
 __global__ void __launch_bounds__(256) k_chg_mark(Scratch s, const Globals* g, uint32_t E, uint32_t epoch, ChgLog c) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E || WIN_REJECTED(g) || s.code[i] != TB_CT_OK) return;
+  // (a window the fused pass committed left no scratch columns: its marks are in fmark)
+  if (i >= E || WIN_REJECTED(g) || SP_DONE(g) || s.code[i] != TB_CT_OK) return;
   if (!XFER) return;  // new accounts are the store slice
   const uint32_t dr = s.dr_slot[i], cr = s.cr_slot[i];
   // a post/void of a pending transfer created in this window may carry no slots: its creator,
@@ -37,10 +42,18 @@ __global__ void __launch_bounds__(256) k_chg_mark(Scratch s, const Globals* g, u
   if ((s.cls[i] & C_POSTVOID) && s.p_tslot[i] != NONE32) c.pend[atomicAdd(&c.cnt[1], 1u)] = s.p_tslot[i];
 }
 
+// Whether account `slot` changed in log `epoch` (the general path's marks, or the fused pass's when it
+// committed that window).
+__device__ inline bool chg_marked(const Globals* g, const ChgLog& c, uint64_t slot, uint32_t epoch) {
+  if (slot >= g->acc_count) return false;
+  if (c.mark[slot] == epoch) return true;
+  return g->sp_done && g->fu_epoch == epoch && c.fmark[slot] == epoch;
+}
+
 __global__ void __launch_bounds__(SEG) k_chg_count(Dev d, uint32_t epoch, ChgLog c) {
   __shared__ uint32_t lds[SEG / 64];
   const uint64_t slot = (uint64_t)blockIdx.x * SEG + threadIdx.x;
-  const uint32_t m = (slot < d.g->acc_count && c.mark[slot] == epoch) ? 1u : 0u;
+  const uint32_t m = chg_marked(d.g, c, slot, epoch) ? 1u : 0u;
   const uint32_t tot = block_sum<SEG / 64>(m, lds);
   if (threadIdx.x == 0) c.seg[blockIdx.x] = tot;
 }
@@ -63,10 +76,21 @@ __global__ void __launch_bounds__(1024) k_chg_scan(uint32_t nseg, ChgLog c) {
 __global__ void __launch_bounds__(SEG) k_chg_list(Dev d, uint32_t epoch, ChgLog c) {
   __shared__ uint32_t lds[SEG / 64];
   const uint64_t slot = (uint64_t)blockIdx.x * SEG + threadIdx.x;
-  const bool m = slot < d.g->acc_count && c.mark[slot] == epoch;
+  const bool m = chg_marked(d.g, c, slot, epoch);
   uint32_t tot;
   const uint32_t r = c.seg[blockIdx.x] + block_excl<SEG / 64>(m ? 1u : 0u, lds, &tot);
   if (m) c.list[r] = (uint32_t)slot;
+}
+
+// Zeroes a log's counters at the start of a commit call, except while a fused-only window waits for
+// its replay (window_error bit 3): its pulse already listed its expiries here, and the replay keeps
+// that log (host.inc settle()).
+__global__ void k_chg_begin(const Globals* g, ChgLog c) {
+  if (g->window_error & 8u) return;
+  c.cnt[0] = 0;
+  c.cnt[1] = 0;
+  c.cnt[2] = 0;
+  c.cnt[3] = 0;
 }
 
 // Gathers the changed account records and the resolved pending transfers' rows.

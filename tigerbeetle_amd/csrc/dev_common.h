@@ -119,12 +119,11 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t x_sorted;
   uint32_t win_flags;   // this transfer window (k_prep_reduce): bit 0 claim-free, bit 1 extends the prefix
   uint32_t mono_prev;   // the previous transfer window was claim-free (k_ct_prep's speculation)
-  uint64_t x_id_max;    // >= every stored transfer id (u64 max once any id needs > 64 bits): an id
-                        // above it cannot exist, so its table probe is skipped (monotonic ids)
+  u128 x_id_max;        // >= every stored transfer id (u128 order): an id above it cannot exist, so its
+                        // table probe is skipped (strictly increasing ids, 64- or 128-bit)
   uint64_t windows_applied;  // create_* windows applied (rejected windows excluded), cumulative
   uint32_t final_done;  // k_final blocks finished in a window with pulse_next ops (the last runs k_pn)
   uint32_t pad4;
-  uint64_t win_id_max;  // this window's largest transfer id key (k_ct_prep), folded into x_id_max
   // chunked resolver (chunks.h), per window: hot accounts left after k_bind_decide (compact ranks
   // 0..hot_live-1) and whether this window's resolver runs in chunked mode
   uint32_t hot_live;
@@ -148,6 +147,7 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t fu_fail_epoch;  // the fused-only window that left the class (window_error bit 3)
   uint32_t sh_mis;         // sharded: this shard's ledger-mismatch slots used this window (shard.h)
   uint32_t sh_unsup;       // sharded: a home event outside the class this window (k_sh_count -> trailer 2)
+  uint64_t ovf_rescans;    // times ovf_bound was re-tightened to the accounts' largest balance sum (restore.h)
 };
 
 // The fused pass (fused.h) committed this window: the general path's kernels return at once.
@@ -283,23 +283,41 @@ __device__ inline uint32_t x_find(const XEntry* __restrict__ tab, const tb_trans
   return x_probe_from(tab, xr, mask, h, tab[h & mask], id);
 }
 
-// Binary search of the sorted transfer prefix [0, P) (Globals::x_sorted).
+// Binary search of the sorted transfer prefix [0, P) (Globals::x_sorted), in u128 id order.
 __device__ inline uint32_t x_prefix_find(const tb_transfer_t* __restrict__ xr, uint64_t P, tb_uint128_t id) {
-  if (P == 0 || id.hi != 0) return NONE32;
+  if (P == 0) return NONE32;
+  const u128 key = U(id);
   uint64_t lo = 0, hi = P;
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    if (xr[mid].id.lo < id.lo)
+    if (U(xr[mid].id) < key)
       lo = mid + 1;
     else
       hi = mid;
   }
-  return (lo < P && xr[lo].id.lo == id.lo) ? (uint32_t)lo : NONE32;
+  return (lo < P && U(xr[lo].id) == key) ? (uint32_t)lo : NONE32;
 }
 
 // Whether `id` can be in the transfer table (x_id_max bounds every stored id).
-__device__ inline bool x_may_exist(const tb_uint128_t& id, uint64_t x_id_max) { return id.hi != 0 || id.lo <= x_id_max; }
-__device__ inline uint64_t x_id_key(const tb_uint128_t& id) { return id.hi ? ~0ull : id.lo; }
+__device__ inline bool x_may_exist(const tb_uint128_t& id, u128 x_id_max) { return U(id) <= x_id_max; }
+__device__ inline u128 umax128(u128 a, u128 b) { return a > b ? a : b; }
+// Raises a u128 upper bound with two 64-bit atomics: the word-wise maximum is >= every value offered
+// (for rare paths: open, sharded apply); the hot paths fold exact per-block maxima instead.
+__device__ inline void atomic_bound_u128(u128* p, u128 v) {
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(p);
+  atomicMax(w, (unsigned long long)v);
+  atomicMax(w + 1, (unsigned long long)(v >> 64));
+}
+// Wave-wide max of a u128 (every lane gets it).
+__device__ inline u128 wave_max_u128(u128 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t lo = __shfl_xor((unsigned long long)v, o, 64), hi = __shfl_xor((unsigned long long)(v >> 64), o, 64);
+    const u128 y = ((u128)hi << 64) | lo;
+    v = y > v ? y : v;
+  }
+  return v;
+}
 
 // Inserts of distinct, absent keys: claim by CAS on the slot word, then publish the key. Readers
 // run in later kernels only.

@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   __shared__ uint4 stage[256 * 4];  // half of each event's record (16 KiB): the in-place record store
   // bit 0 huge amount, bit 1 not claim-free, bit 2 first id above every stored id, bit 3 pulse_next op
   __shared__ uint32_t aux;
-  __shared__ unsigned long long id_max;  // largest id key this block may insert (Globals::x_id_max)
+  __shared__ u128 id_max[256 / 64];  // per wave: largest id this block may insert (Globals::x_id_max)
   __shared__ uint32_t marked[MARK_LDS];  // mark_first: accounts this block marks
   __shared__ uint32_t nfirst, fbase;      // accounts this block marked first, their first rank
   if (WIN_REJECTED(d.g) || SP_DONE(d.g)) return;
@@ -239,7 +239,6 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   for (uint32_t j = threadIdx.x; j < MARK_LDS; j += blockDim.x) marked[j] = NONE32;
   if (threadIdx.x == 0) {
     aux = 0;
-    id_max = 0;
     nfirst = 0;
   }
   __syncthreads();
@@ -247,8 +246,9 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   u128 amount_upper = 0;
   tb_transfer_t t;  // the event, stamped (also the record a plain create stores in place)
   bool prec = false;
+  u128 my_id = 0;  // the id, if the event reaches the exists check (an upper bound of what it may store)
   if (i < w.E) {
-    const uint64_t x_id_max = d.g->x_id_max;
+    const u128 x_id_max = d.g->x_id_max;
     const uint64_t P = d.g->x_sorted;
     // speculation: claim-free like the previous window (k_claim_fix claims if it was not)
     const bool spec = d.g->mono_prev != 0;
@@ -256,11 +256,11 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     const uint8_t* evb = reinterpret_cast<const uint8_t*>(ev);
     const uint32_t b = win_batch(w, i);
     {
-      // claim-free: ids strictly increasing over the window, all < 2^64, no post/void
-      bool nf = t.id.hi != 0 || (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
-      if (i > 0) nf |= !(t.id.lo > ev[i - 1].id.lo);
+      // claim-free: ids strictly increasing (u128 order) over the window, no post/void
+      bool nf = (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+      if (i > 0) nf |= !(U(t.id) > U(ev[i - 1].id));
       if (nf) atomicOr(&aux, 2u);
-      if (i == 0 && t.id.hi == 0 && t.id.lo > x_id_max) atomicOr(&aux, 4u);
+      if (i == 0 && U(t.id) > x_id_max) atomicOr(&aux, 4u);
     }
     uint32_t cls = 0, code;
     uint32_t dr_slot = NONE32, cr_slot = NONE32, id_tslot = NONE32, p_tslot = NONE32, id_ent = NONE32,
@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
       atomicOr(&aux, 8u);
     }
     if (cls & C_HIST) atomicOr(&aux, 32u);
-    if (cls & C_REACH) atomicMax(&id_max, (unsigned long long)x_id_key(t.id));
+    if (cls & C_REACH) my_id = U(t.id);
     if ((i & (SEG - 1)) == 0) {  // the segment counts k_classify accumulates
       s.cnt_w[i / SEG] = 0;
       s.cnt_bad[i / SEG] = 0;
@@ -470,6 +470,10 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
       if (f1) hot_rank_set(d, s, first_slot[1], fbase + k1);
     }
   }
+  {
+    const u128 wm = wave_max_u128(my_id);
+    if ((threadIdx.x & 63) == 0) id_max[threadIdx.x >> 6] = wm;
+  }
   red[threadIdx.x] = ((uint64_t)(amount_upper >> 64) != 0) ? 0 : amount_upper;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
@@ -479,8 +483,11 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
   if (threadIdx.x == 0) {
     s.blk_amt[blockIdx.x] = red[0];
     s.blk_aux[blockIdx.x] = aux;
-    // an upper bound of every id this window may store (the failures' ids included)
-    if (id_max) atomicMax(reinterpret_cast<unsigned long long*>(&d.g->win_id_max), id_max);
+    // an upper bound of every id this window may store (the failures' ids included; k_prep_reduce
+    // folds the blocks' exact maxima)
+    u128 m = id_max[0];
+    for (int q = 1; q < 256 / 64; q++) m = umax128(m, id_max[q]);
+    s.blk_idmax[blockIdx.x] = m;
   }
 }
 
@@ -498,18 +505,22 @@ __device__ inline u128 block_sum_u128(u128 v, u128* lds) {
 
 __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t nblk) {
   __shared__ u128 red[1024];
+  __shared__ u128 idm[1024 / 64];
   __shared__ uint32_t aux;
   if (WIN_REJECTED(d.g) || SP_DONE(d.g)) return;
   if (threadIdx.x == 0) aux = 0;
   __syncthreads();
-  u128 v = 0;
+  u128 v = 0, m = 0;
   uint32_t a = 0;
   for (uint32_t j = threadIdx.x; j < nblk; j += 1024) {
     v += s.blk_amt[j];
     a |= s.blk_aux[j];
+    m = umax128(m, s.blk_idmax[j]);
   }
   if (a) atomicOr(&aux, a);
-  const u128 tot = block_sum_u128(v, red);
+  m = wave_max_u128(m);
+  if ((threadIdx.x & 63) == 0) idm[threadIdx.x >> 6] = m;
+  const u128 tot = block_sum_u128(v, red);  // (its barriers order the idm stores)
   if (threadIdx.x == 0) {
     Globals* g = d.g;
     g->batch_amount_sum += tot;
@@ -525,8 +536,9 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
     // component walkers, which run before k_walk, read it from here)
     const u128 sum = g->ovf_bound + g->batch_amount_sum;
     g->small_win = !g->batch_huge && sum >= g->ovf_bound && (uint64_t)(sum >> 64) == 0;
-    if (g->win_id_max > g->x_id_max) g->x_id_max = g->win_id_max;
-    g->win_id_max = 0;
+    u128 wm = idm[0];
+    for (int q = 1; q < 1024 / 64; q++) wm = umax128(wm, idm[q]);
+    if (wm > g->x_id_max) g->x_id_max = wm;
   }
 }
 

@@ -13,8 +13,9 @@
 //
 // Simple = every event of the window is either decided statically (validation, lookups, ledgers,
 // exists) or is a plain create (no linked / pending / post / void / balancing flag) whose accounts
-// carry no limit and no history flag, every id is below 2^64 and strictly increasing over the window
-// (so no id repeats: the window is claim-free), and every amount reaching the account checks is below
+// carry no limit and no history flag, the ids are strictly increasing over the window in u128 order
+// (64-bit sequences and the reference's time-based 128-bit ids alike, docs/develop/data-modeling.md:
+// 186-203; so no id repeats: the window is claim-free), and every amount reaching the account checks is below
 // 2^43 with the overflow bound below 2^63 (so no balance field leaves its low 64-bit word: the
 // overflow checks of :1532-1545 cannot fail, and the balance adds are exact no-return 64-bit adds).
 // Then every outcome is a function of the pre-window state and the event alone.
@@ -31,15 +32,6 @@
 
 #define FU_T 256
 #define FU_AMOUNT_MAX (1ull << 43)  // per-event amount bound: 2^20 events x 2^43 <= 2^63
-// timing experiments only (results wrong): 1 no balance adds, 4 no record stores
-#ifndef FU_EXP
-#define FU_EXP 0
-#endif
-// event loads: 0 per lane (8 strided 16 B loads), 1 staged through LDS in 64 B halves, 2 the same
-// nontemporal (the stream passes by; the account table and records stay in the Infinity Cache)
-#ifndef FU_STAGE
-#define FU_STAGE 2
-#endif
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
@@ -61,21 +53,21 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 struct FuEv {
   uint32_t code, dr, cr;
   unsigned long long amount;  // C_REACH events: the amount (every one counts toward the overflow bound)
-  unsigned long long id_key;  // C_REACH events: the id (x_id_max bound)
+  u128 id_key;                // C_REACH events: the id (x_id_max bound)
   bool simple, reach;
 };
 
-// prev_id_lo: the id of event i - 1 (i > 0).
-__device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, uint64_t prev_id_lo, const tb_transfer_t& t,
-                                          uint64_t x_id_max, uint64_t P, FuEv* o) {
+// prev_id: the id of event i - 1 (i > 0).
+__device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id, const tb_transfer_t& t,
+                                          u128 x_id_max, uint64_t P, FuEv* o) {
   const uint16_t f = t.flags;
   o->dr = o->cr = NONE32;
   o->amount = 0;
   o->id_key = 0;
   o->reach = false;
-  // claim-free: ids strictly increasing over the window, below 2^64, no post/void (k_ct_prep's test)
-  bool simple = !(f & TB_TRANSFER_LINKED) && t.id.hi == 0 && !(f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
-  if (i > 0) simple = simple && t.id.lo > prev_id_lo;
+  // claim-free: ids strictly increasing over the window, no post/void (k_ct_prep's test)
+  bool simple = !(f & TB_TRANSFER_LINKED) && !(f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
+  if (i > 0) simple = simple && U(t.id) > prev_id;
   uint32_t code;
   if (t.timestamp != 0) {
     code = TB_CT_TIMESTAMP_MUST_BE_ZERO;  // :1251
@@ -107,7 +99,7 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, uint64_t pre
           if (code == CONT) {
             o->reach = true;
             o->amount = t.amount.lo;
-            o->id_key = t.id.lo;
+            o->id_key = U(t.id);
             // a limit or history flag reads (or records) balances in order: not order-free
             if (((de.flags | ce.flags) & TB_ACCOUNT_HISTORY) || (de.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) ||
                 (ce.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) || t.amount.hi != 0 || t.amount.lo >= FU_AMOUNT_MAX)
@@ -128,7 +120,8 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, uint64_t pre
 // Scratch of the fused pass (per 256-event block; per 64-event wave).
 struct FuScratch {
   uint32_t* cnt;            // per block: failed events
-  unsigned long long* pay;  // per block: [2k] its reaching amounts' sum, [2k+1] its largest reaching id
+  unsigned long long* pay;  // per block: its reaching amounts' sum
+  u128* idmax;              // per block: its largest reaching id
   uint8_t* applied;         // per block: its balance adds were applied (k_fu_final undoes them)
   unsigned long long* ok;   // per wave: ok-event bitmap
 };
@@ -161,20 +154,31 @@ __device__ __forceinline__ void fu_store_records(Dev d, const tb_transfer_t& t, 
 // Decide, apply, store in place. Writes nothing but scratch, the in-place records and statuses (slots
 // at or beyond the store's end) and, when its events are simple, the balance adds.
 __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
-                                                   WinDesc w, uint32_t epoch) {
+                                                   WinDesc w, uint32_t epoch, uint32_t fo_only, uint32_t* fmark) {
   __shared__ uint4 stage[FU_T * 4];  // half of each inserted record per round (16 KiB)
   __shared__ uint32_t lds[FU_T / 64];
-  __shared__ unsigned long long ldsu[2 * (FU_T / 64)];
+  __shared__ unsigned long long ldsu[FU_T / 64];
+  __shared__ u128 ldsm[FU_T / 64];
+  __shared__ uint32_t aborted_lds;
   Globals* g = d.g;
   if (WIN_REJECTED(g)) return;
   const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (g->sp_skip) {  // backed off: the general path decides this window
-    if (k == 0 && threadIdx.x == 0) g->sp_done = 0;
+    if (k == 0 && threadIdx.x == 0) {
+      g->sp_done = 0;
+      // a fused-only window has no general path behind it (a non-fused-only window outside the class
+      // left the back-off on): hand it to settle()'s replay like a window found outside the class
+      if (fo_only) {
+        g->fu_fail_epoch = epoch;
+        atomicOr(&g->window_error, 8u);
+      }
+    }
     return;
   }
   const uint32_t i = k * FU_T + threadIdx.x;
   const uint32_t E = w.E;
-  const uint64_t base = g->x_count, x_id_max = g->x_id_max, P = g->x_sorted;
+  const uint64_t base = g->x_count, P = g->x_sorted;
+  const u128 x_id_max = g->x_id_max;
   const u128 ovf = g->ovf_bound;
   // window-level condition: the balance fields stay below 2^64 (ovf + 2^20 x 2^43 < 2^64)
   const bool glob_ok = (uint64_t)(ovf >> 64) == 0 && (uint64_t)ovf < (1ull << 63) && !g->batch_huge;
@@ -183,9 +187,14 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
     g->fu_epoch = epoch;
     g->fu_base = base;
     // the window extends the sorted prefix (claim-free when simple; first id above every stored id)
-    g->fu_prefix = (P == base && ev[0].id.hi == 0 && ev[0].id.lo > x_id_max) ? 1u : 0u;
+    g->fu_prefix = (P == base && U(ev[0].id) > x_id_max) ? 1u : 0u;
   }
-  const bool aborted = __hip_atomic_load(&g->fu_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+  // Another block may flag the window at any time: one read per block, so that every wave and
+  // fs.applied[k] agree on whether this block applies its adds (k_fu_final undoes exactly those).
+  if (threadIdx.x == 0)
+    aborted_lds = __hip_atomic_load(&g->fu_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch ? 1u : 0u;
+  __syncthreads();
+  const bool aborted = aborted_lds != 0;
 
   tb_transfer_t t;
   FuEv fe;
@@ -194,11 +203,11 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   fe.code = TB_CT_OK;
   fe.amount = fe.id_key = 0;
   fe.dr = fe.cr = NONE32;
-  uint64_t prev = 0;
-#if FU_STAGE
+  u128 prev = 0;
   if (!aborted) {
     // the wave's 64 records through LDS in two 64 B halves (16 B per lane per load, row-swizzled so
-    // the per-lane row reads are conflict-free)
+    // the per-lane row reads are conflict-free), nontemporal: the stream passes by while the account
+    // table and records stay in the Infinity Cache (per-lane strided loads measured slower)
     uint4* ws = stage + wave * 256;
     const uint32_t i0 = i - lane;
     const uint32_t nrec = i0 < E ? min(64u, E - i0) : 0u;
@@ -210,23 +219,17 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
 #pragma unroll
       for (int c = 0; c < 4; c++) {
         const uint32_t idx = c * 64 + lane, r = idx >> 2, q = idx & 3;
-        if (r < nrec) ws[r * 4 + (q ^ ((r >> 2) & 3))] = FU_STAGE == 2 ? ld_stream(src + r * 8 + half * 4 + q)
-                                                                        : src[r * 8 + half * 4 + q];
+        if (r < nrec) ws[r * 4 + (q ^ ((r >> 2) & 3))] = ld_stream(src + r * 8 + half * 4 + q);
       }
       wave_sync();
 #pragma unroll
       for (int q = 0; q < 4; q++) tw[half * 4 + q] = ws[lane * 4 + (q ^ ((lane >> 2) & 3))];
     }
-    // the previous event's id: the neighbour lane's (lane 0: the previous wave's last event)
-    prev = __shfl_up(t.id.lo, 1, 64);
-    if (lane == 0 && i > 0) prev = ev[i - 1].id.lo;
+    // the previous event's id: the neighbour lane's (lane 0: the previous wave's last event; a wave
+    // wholly past the window's end reads nothing, ev ends at E)
+    prev = ((u128)__shfl_up(t.id.hi, 1, 64) << 64) | __shfl_up(t.id.lo, 1, 64);
+    if (lane == 0 && i > 0 && i < E) prev = U(ev[i - 1].id);
   }
-#else
-  if (i < E && !aborted) {
-    t = ev[i];
-    if (i > 0) prev = ev[i - 1].id.lo;
-  }
-#endif
   if (i < E && !aborted) {
     fu_decide(d, i, prev, t, x_id_max, P, &fe);
     t.timestamp = win_ts(w, win_batch(w, i), i);  // :1253 (the record as inserted)
@@ -239,42 +242,49 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   }
   if (!blk_simple) return;
   const bool ok = i < E && fe.code == TB_CT_OK;
-  if (ok && !(FU_EXP & 1)) {
+  if (ok) {
     // no-return 64-bit adds: every field stays below 2^64 this window (glob_ok, FU_AMOUNT_MAX)
     (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.dr].debits_posted), fe.amount);
     (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.cr].credits_posted), fe.amount);
+    if (fmark) {
+      // write-back stream (changes.h): the accounts this window changed, tagged with its number;
+      // counted only if the pass commits the window (k_chg_count)
+      fmark[fe.dr] = epoch;
+      fmark[fe.cr] = epoch;
+    }
   }
   const bool bad = i < E && !ok;
   if (bad) s.code[i] = fe.code;
   const unsigned long long okm = __ballot(ok);
   if (lane == 0 && i < E) fs.ok[i >> 6] = okm;
   if (ok) d.xstatus[base + i] = 0;
-  if (okm && !(FU_EXP & 4)) {  // in place: slot base + i
+  if (okm) {  // in place: slot base + i
     const uint32_t first = (uint32_t)__builtin_ctzll(okm);
     fu_store_records(d, t, ok, okm, base + (i - lane) + first, stage + wave * 256);
   }
   // this block's failures, reaching amounts' sum and largest reaching id (k_fu_final folds them)
   const uint32_t wbad = (uint32_t)__popcll(__ballot(bad));
   const unsigned long long wsum = wave_sum_u64(fe.reach ? fe.amount : 0ull);
-  const unsigned long long wmax = wave_max_u64(fe.reach ? fe.id_key : 0ull);
+  const u128 wmax = wave_max_u128(fe.reach ? fe.id_key : (u128)0);
   if (lane == 0) {
     lds[wave] = wbad;
-    ldsu[2 * wave] = wsum;
-    ldsu[2 * wave + 1] = wmax;
+    ldsu[wave] = wsum;
+    ldsm[wave] = wmax;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t nbad = 0;
-    unsigned long long bsum = 0, bmax = 0;
+    unsigned long long bsum = 0;
+    u128 bmax = 0;
 #pragma unroll
     for (uint32_t q = 0; q < FU_T / 64; q++) {
       nbad += lds[q];
-      bsum += ldsu[2 * q];
-      bmax = ldsu[2 * q + 1] > bmax ? ldsu[2 * q + 1] : bmax;
+      bsum += ldsu[q];
+      bmax = umax128(bmax, ldsm[q]);
     }
     fs.cnt[k] = nbad;
-    fs.pay[2 * k] = bsum;
-    fs.pay[2 * k + 1] = bmax;
+    fs.pay[k] = bsum;
+    fs.idmax[k] = bmax;
     if (nbad) {
       // the window's failure count, tagged with its epoch (no reset between windows)
       unsigned long long* acc = reinterpret_cast<unsigned long long*>(&g->fu_bad);
@@ -301,7 +311,8 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
                                                    WinDesc w, uint32_t epoch, FinalOut o, uint32_t fo_only) {
   __shared__ uint4 stage[FU_T * 4];
   __shared__ uint32_t lds[FU_T / 64];
-  __shared__ unsigned long long red[2 * (FU_T / 64)];
+  __shared__ unsigned long long red[FU_T / 64];
+  __shared__ u128 redm[FU_T / 64];
   Globals* g = d.g;
   // (bit 0 only: this kernel itself may set bit 3, and every block must still undo its adds)
   if ((g->window_error & 1u) || g->fu_epoch != epoch) return;  // (k_ct_fused backed off or skipped)
@@ -320,7 +331,7 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
     }
     if (!fs.applied[k] || i >= E) return;
     FuEv fe;
-    fu_decide(d, i, i > 0 ? ev[i - 1].id.lo : 0ull, ev[i], g->x_id_max, g->x_sorted, &fe);
+    fu_decide(d, i, i > 0 ? U(ev[i - 1].id) : (u128)0, ev[i], g->x_id_max, g->x_sorted, &fe);
     if (fe.code == TB_CT_OK) {
       (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.dr].debits_posted), 0ull - fe.amount);
       (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.cr].credits_posted), 0ull - fe.amount);
@@ -377,22 +388,23 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
   if (ok && !prefix_win) x_insert(d.x_tab, d.x_mask, ev[i].id, (uint32_t)(base + rins));
   if (k == gridDim.x - 1) {
     // the window's totals: the per-block sums folded, the store counts and the window state
-    unsigned long long sum = 0, mx = 0;
+    unsigned long long sum = 0;
+    u128 mx = 0;
     for (uint32_t j = threadIdx.x; j < gridDim.x; j += FU_T) {
-      sum += fs.pay[2 * j];
-      mx = fs.pay[2 * j + 1] > mx ? fs.pay[2 * j + 1] : mx;
+      sum += fs.pay[j];
+      mx = umax128(mx, fs.idmax[j]);
     }
     sum = wave_sum_u64(sum);
-    mx = wave_max_u64(mx);
+    mx = wave_max_u128(mx);
     if (lane == 0) {
-      red[2 * wave] = sum;
-      red[2 * wave + 1] = mx;
+      red[wave] = sum;
+      redm[wave] = mx;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
       for (uint32_t q = 1; q < FU_T / 64; q++) {
-        sum += red[2 * q];
-        mx = red[2 * q + 1] > mx ? red[2 * q + 1] : mx;
+        sum += red[q];
+        mx = umax128(mx, redm[q]);
       }
       const uint32_t total_ins = E - total_bad;
       for (int32_t bb = (int32_t)w.nb; bb >= 0 && w.off[bb] == E; bb--) o.batch_base[bb] = total_bad;

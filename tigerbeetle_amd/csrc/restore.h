@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(256) k_load_transfers(Dev d, uint64_t first, u
     const uint64_t slot = first + k;
     const tb_transfer_t t = d.xr[slot];
     x_insert(d.x_tab, d.x_mask, t.id, (uint32_t)slot);
-    atomicMax(reinterpret_cast<unsigned long long*>(&d.g->x_id_max), (unsigned long long)x_id_key(t.id));
+    atomic_bound_u128(&d.g->x_id_max, U(t.id));
     if (!(t.flags & TB_TRANSFER_PENDING) || t.timeout == 0 || d.xstatus[slot] != TB_PENDING_PENDING) continue;
     const uint64_t expires_at = expires_at_of(t);
     if ((t.timestamp >> 63) || expires_at > TB_TIMESTAMP_MAX) continue;  // never visible to the scan
@@ -89,6 +89,56 @@ __global__ void k_load_finish(Dev d, const LoadBound* lb, uint64_t n_acc, uint64
     g->ovf_bound = ((u128)lb->hi_max << 64) | (u128)~0ull;
   else
     g->ovf_bound = lb->lo_max;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Re-tightening the overflow bound. Globals::ovf_bound only grows while windows commit (each adds its
+// amount sum: it must stay >= every dp+dpo and cp+cpo without reading them), so after enough volume
+// it is far above any real balance sum and the overflow-free fast paths (fused pass: below 2^63;
+// 64-bit no-return adds: below 2^64) would stay off for good. When the host sees it past
+// OVF_RESCAN_AT at a state read, one grid pass sets it to the accounts' largest sum again (the
+// LoadBound rule of open: exact while every sum fits 64 bits).
+// ------------------------------------------------------------------------------------------------
+#define OVF_RESCAN_AT ((u128)1 << 62)
+
+__global__ void __launch_bounds__(256) k_ovf_rescan(Dev d, uint64_t n, LoadBound* lb) {
+  __shared__ unsigned long long lh[256 / 64], ll[256 / 64];
+  unsigned long long hi = 0, lo = 0;
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    const tb_account_t& a = d.acc[k];
+    const u128 dp = U(a.debits_pending), cp = U(a.credits_pending);
+    const u128 s1 = dp + U(a.debits_posted), s2 = cp + U(a.credits_posted);
+    const u128 m = s1 > s2 ? s1 : s2;
+    const unsigned long long h = (s1 < dp || s2 < cp) ? ~0ull : (unsigned long long)(m >> 64);
+    if (h) hi = h > hi ? h : hi;
+    else lo = (unsigned long long)m > lo ? (unsigned long long)m : lo;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(hi, o, 64), z = __shfl_xor(lo, o, 64);
+    hi = y > hi ? y : hi;
+    lo = z > lo ? z : lo;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    lh[threadIdx.x >> 6] = hi;
+    ll[threadIdx.x >> 6] = lo;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 256 / 64; q++) {
+      hi = lh[q] > hi ? lh[q] : hi;
+      lo = ll[q] > lo ? ll[q] : lo;
+    }
+    if (hi) atomicMax(&lb->hi_max, hi);
+    if (lo) atomicMax(&lb->lo_max, lo);
+  }
+}
+
+__global__ void k_ovf_finish(Dev d, const LoadBound* lb) {
+  Globals* g = d.g;
+  if (g->window_error) return;  // (the host reads again after a reported or replayed window)
+  g->ovf_bound = lb->hi_max == ~0ull ? MAX128 : lb->hi_max ? (((u128)lb->hi_max << 64) | (u128)~0ull) : (u128)lb->lo_max;
+  g->ovf_rescans++;
 }
 
 // ------------------------------------------------------------------------------------------------

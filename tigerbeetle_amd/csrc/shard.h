@@ -287,10 +287,10 @@ __global__ void __launch_bounds__(SEG) k_sh_roles(Dev d, Scratch s, const uint8_
       if (shard_of(dra.lo, dra.hi, G) == me) roles |= ROLE_DR;
       if (shard_of(cra.lo, cra.hi, G) == me) roles |= ROLE_CR;
       // the owned records extend the sorted prefix if the window's ids are strictly increasing
-      bool nm = id.hi != 0;
-      if (i > 0) nm |= !(id.lo > reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i - 1].id.lo);
+      bool nm = false;
+      if (i > 0) nm = !(U(id) > U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i - 1].id));
       if (nm) atomicOr(&aux, (uint32_t)SHX_NONMONO);
-      if (i == 0 && id.hi == 0 && id.lo > d.g->x_id_max) atomicOr(&aux, (uint32_t)SHX_FRESH);
+      if (i == 0 && U(id) > d.g->x_id_max) atomicOr(&aux, (uint32_t)SHX_FRESH);
       xch.acc[i] = 0;  // k_sh_owned writes the owned facts
     }
     xch.zw[i] = 0;
@@ -632,7 +632,7 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
                                                   const uint32_t* trailer1, const uint32_t* trailer2,
                                                   const unsigned long long* bits, ChgLog chg, uint32_t chg_epoch) {
   __shared__ uint32_t lds[SEG / 64];
-  __shared__ unsigned long long ldsm[SEG / 64];
+  __shared__ u128 ldsm[SEG / 64];
   // inserted transfer records, compacted per wave and stored as one contiguous run (as in k_final)
   __shared__ uint4 stage[XFER ? SEG * 8 : 1];
   Globals* g = d.g;
@@ -659,9 +659,15 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
   uint32_t tot_ins;
   const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
   if (XFER) {
-    const unsigned long long key = ins ? x_id_key(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].id) : 0ull;
-    const unsigned long long m = block_max_u64<SEG / 64>(key, ldsm);
-    if (threadIdx.x == 0 && m > g->x_id_max) atomicMax(reinterpret_cast<unsigned long long*>(&g->x_id_max), m);
+    const u128 key = ins ? U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].id) : (u128)0;
+    const u128 m = wave_max_u128(key);
+    if ((threadIdx.x & 63) == 0) ldsm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      u128 bm = ldsm[0];
+      for (int q = 1; q < SEG / 64; q++) bm = umax128(bm, ldsm[q]);
+      if (bm > g->x_id_max) atomic_bound_u128(&g->x_id_max, bm);
+    }
   }
   const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, 0);  // the wave's first insert rank (all lanes active here)
   if (commit) {

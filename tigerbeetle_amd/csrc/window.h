@@ -92,6 +92,7 @@ struct Scratch {
   // per-block partials reduced by one small kernel (no same-address atomics across blocks)
   u128* blk_amt;                   // prep blocks: sum of the window's amounts
   uint32_t* blk_aux;               // prep blocks: bit 0 huge amount, bit 1 unsupported (sharded), own << 2
+  u128* blk_idmax;                 // prep blocks: largest id that reaches the exists check (x_id_max)
   ExpEntry* cand;
   // account-parallel resolver (resolver.h)
   uint32_t *rkey_in, *rval_in, *rkey, *rval;  // (hot rank, 2*event+side) pairs, then sorted by rank

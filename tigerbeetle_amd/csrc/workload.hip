@@ -340,6 +340,13 @@ extern "C" int tbg_gen_transfers_cfg4(void* d_out, uint64_t first, uint64_t coun
 //   sequential  identity:  data
 //   reversed    inversion: maxInt(u128) - data
 //   random      pseudo-UUID: data << 32 | (Xoshiro256(seed +% data).int(u128) & ~(maxInt(u64) << 32))
+// plus one order the reference benchmark does not have but its docs recommend for every application
+// (docs/develop/data-modeling.md:186-203, the clients' id()):
+//   time        48-bit millisecond timestamp above 80 random bits, the random part incremented for
+//               the ids of the same millisecond: strictly increasing 128-bit ids whose high word is
+//               never zero. The stream's clock advances one millisecond every 2^18 ids (about the
+//               rate of the fused pass); each millisecond draws a fresh random part (below 2^79, so
+//               the increments never carry into the timestamp).
 // Zig std's DefaultPrng is Xoshiro256++ seeded through SplitMix64, and Random.int(u128) reads two
 // next() words little-endian, so the ids are the reference's own for the same permutation seed
 // (benchmark_load.zig:120-125 draws it as the first u64 of DefaultPrng.init(seed)).
@@ -348,6 +355,9 @@ extern "C" int tbg_gen_transfers_cfg4(void* d_out, uint64_t first, uint64_t coun
 // (one bijection for all, so a stream keeps its outcomes under any order).
 // ------------------------------------------------------------------------------------------------
 __host__ __device__ inline uint64_t wl_rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+#define WL_TIME_BASE_MS 1700000000000ull  // (2023-11-14, 48 bits)
+#define WL_TIME_PER_MS_LOG2 18
 
 __host__ __device__ inline tb_uint128_t wl_encode_id(uint64_t data, uint32_t order, uint64_t seed) {
   tb_uint128_t id;
@@ -376,6 +386,12 @@ __host__ __device__ inline tb_uint128_t wl_encode_id(uint64_t data, uint32_t ord
   } else if (order == 2) {
     id.lo = ~data;
     id.hi = ~0ull;
+  } else if (order == 3) {
+    const uint64_t ms = WL_TIME_BASE_MS + ((data - 1) >> WL_TIME_PER_MS_LOG2);
+    const uint64_t k = (data - 1) & ((1ull << WL_TIME_PER_MS_LOG2) - 1);
+    const uint64_t r_lo = wl_rnd(seed, ms, 7), r_hi = wl_rnd(seed, ms, 8) & 0x7FFFull;
+    id.lo = r_lo + k;
+    id.hi = (ms << 16) | (r_hi + (id.lo < r_lo ? 1ull : 0ull));
   } else {
     id.lo = data;
     id.hi = 0;
@@ -398,7 +414,7 @@ __global__ void k_permute_ids(uint8_t* recs, uint64_t count, uint32_t transfers,
 
 extern "C" int tbg_gen_permute_ids(void* d_records, uint64_t count, uint32_t transfers, uint32_t order, uint64_t seed,
                                    void* stream) {
-  if (order > 2) return -1;
+  if (order > 3) return -1;
   if (!count || order == 0) return 0;
   k_permute_ids<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>((uint8_t*)d_records, count,
                                                                                 transfers, order, seed);

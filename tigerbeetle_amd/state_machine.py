@@ -77,13 +77,17 @@ class StateMachine:
         return bool(needed.value)
 
     def prefetch(self, op, operation, data):
+        self._pf_data = data
         self._pf = np.frombuffer(data, np.uint8) if data else np.zeros(0, np.uint8)
         ptr = self._pf.ctypes.data if len(data) else None
         _lib.check(_lib.lib().tbg_prefetch(self.h, op, int(operation), ptr, len(data), self.prefetch_timestamp),
                    "prefetch")
 
     def commit(self, client, op, timestamp, operation, data):
-        buf = self._pf if getattr(self, "_pf", None) is not None and self._pf.tobytes() == data else (
+        # the prefetched request (the same buffer, so tbg_commit finds its prefetch)
+        pf = getattr(self, "_pf", None)
+        same = pf is not None and (data is self._pf_data or pf.tobytes() == data)
+        buf = pf if same else (
             np.frombuffer(data, np.uint8) if data else np.zeros(0, np.uint8))
         ptr = buf.ctypes.data if len(data) else None
         n = ctypes.c_uint64()

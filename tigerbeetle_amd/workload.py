@@ -205,7 +205,9 @@ def transfers_cfg4(first, count, seed, n_accounts, batch, id_offset=0):
 # IdPermutation.encode (testing/id.zig:8-48) with Zig std's DefaultPrng (Xoshiro256++, SplitMix64
 # seeding).
 # ------------------------------------------------------------------------------------------------
-ID_ORDERS = {"sequential": 0, "random": 1, "reversed": 2}
+ID_ORDERS = {"sequential": 0, "random": 1, "reversed": 2, "time": 3}
+TIME_BASE_MS = 1700000000000
+TIME_PER_MS_LOG2 = 18
 _M64 = (1 << 64) - 1
 
 
@@ -253,6 +255,16 @@ def encode_ids(data, order, seed=0):
         return data.copy(), np.zeros_like(data)
     if order == 2:
         return ~data, np.full_like(data, np.uint64(_M64))
+    if order == 3:  # time-based ids (workload.hip wl_encode_id)
+        with np.errstate(over="ignore"):
+            d1 = data - np.uint64(1)
+            ms = np.uint64(TIME_BASE_MS) + (d1 >> np.uint64(TIME_PER_MS_LOG2))
+            k = d1 & np.uint64((1 << TIME_PER_MS_LOG2) - 1)
+            r_lo = rnd(seed, ms, 7)
+            r_hi = rnd(seed, ms, 8) & np.uint64(0x7FFF)
+            lo = r_lo + k
+            hi = (ms << np.uint64(16)) | (r_hi + (lo < r_lo).astype(np.uint64))
+        return lo, hi
     with np.errstate(over="ignore"):
         s = _splitmix_seed(data + np.uint64(seed))
     r0 = _xoshiro_next(s)
