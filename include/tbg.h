@@ -287,6 +287,25 @@ int tbg_aof_replay(tbg_engine *engine, const void *h_aof, uint64_t size, uint32_
 uint64_t tbg_shard_gather_bytes(uint32_t n_events, uint32_t shard_count, uint32_t batch_max, uint64_t *phase2_offset);
 int tbg_shard_gather(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_events,
                      uint64_t timestamp, uint32_t phase, void *d_buffer);
+/* The general class a whole window at a time (replaces one gather round per batch): phase 1 gathers
+ * the accounts and stored transfers every event of the window names and EVERY live entry due at or
+ * before t_last (the window's last batch timestamp), up to due_cap per shard (the shard's count in the
+ * buffer's first bytes: uint32 word shard_index, 0xFFFFFFFF when it had more: the window then goes
+ * batch by batch), plus each shard's smallest live entry beyond t_last; phase 2 the accounts of the
+ * gathered pending and due transfers. Asynchronous, no host round trip. After both sums,
+ * tbg_gathered_objects writes the distinct gathered objects in timestamp order (sorted and
+ * deduplicated on the device; synchronous: the counts size the scratch engine's tbg_open_device),
+ * the scratch engine commits the whole window (tbg_commit_window: the pulses inside it modelled as on
+ * one engine, or TBG_E_WINDOW at tbg_sync, then nothing is applied and the window goes batch by
+ * batch), and tbg_shard_apply keeps the owned objects. Replaces tbg_shard_gather per batch; the
+ * same buffer rules (256-byte aligned, one writer per slot). */
+uint64_t tbg_shard_gather_window_bytes(uint32_t n_events, uint32_t shard_count, uint32_t due_cap,
+                                       uint64_t *phase2_offset);
+int tbg_shard_gather_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_events,
+                            uint64_t t_last, uint32_t phase, void *d_buffer, uint32_t due_cap);
+int tbg_gathered_objects(tbg_engine *engine, const void *d_buffer, uint32_t n_events, uint32_t due_cap,
+                         void *d_accounts, uint64_t *n_accounts, void *d_transfers, uint8_t *d_status,
+                         uint64_t *n_transfers);
 /* d_history / d_history_side (tbg_device_history of the scratch engine, may be NULL): the history
  * row beside each of d_transfers, kept with the transfers this shard inserts. With
  * TBG_FLAG_CHANGE_LOG the shard's write-back stream (tbg_window_changes) then lists what changed on

@@ -468,7 +468,8 @@ def test_fused_resumes_after_overflow_bound_passes_2_63():
         assert st0["fused_windows"] < 132  # the bound passed 2^63 inside the queue
         for h, r in outs:
             assert _replies(h) == r
-        assert st0["ovf_rescans"] == 0
+        # (the sync's state read on the drained stream already re-tightened the bound)
+        assert st0["ovf_rescans"] >= 1
         outs = []
         for w in range(6):
             b = win()
@@ -478,7 +479,6 @@ def test_fused_resumes_after_overflow_bound_passes_2_63():
         for h, r in outs:
             assert _replies(h) == r
         st1 = gpu.stats()
-        assert st1["ovf_rescans"] >= 1
         assert st1["fused_windows"] >= st0["fused_windows"] + 3  # back on the fused pass
         _compare_final(gpu, ref)
     finally:

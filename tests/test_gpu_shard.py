@@ -16,10 +16,16 @@ from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE, Operation
 BM = 8190
 
 
+def same_pulse_log(got, want):
+    """pulse() logs equal, where the sharded one observed it (None: modelled inside a general window)."""
+    return len(got) == len(want) and all(t == u and (p is None or p == q) for (t, p), (u, q) in zip(got, want))
+
+
 class LocalShards:
     """G shards of one engine on cuda:0, driven like one StateMachine (harness timestamps)."""
 
-    def __init__(self, G, batch_max, accounts_max, transfers_max, window_events_max, change_log=False):
+    def __init__(self, G, batch_max, accounts_max, transfers_max, window_events_max, change_log=False,
+                 general="window"):
         from tigerbeetle_amd.sharding import ShardedStateMachine
 
         self.shards = [ShardedStateMachine(G, r, None, batch_max=batch_max, accounts_max=accounts_max,
@@ -27,7 +33,12 @@ class LocalShards:
                                            change_log=change_log)
                        for r in range(G)]
         self.prepare_timestamp = 0
-        self.pulse_log = []  # (T, pulse()) before every batch, the harness order (:2719-2739)
+        # (T, pulse()) before every batch, the harness order (:2719-2739); None where a general window
+        # models the pulse inside it (not observable from outside)
+        self.pulse_log = []
+        # windows outside the order-free class: "window" = one read set per window (commit_general_window),
+        # "batch" = batch by batch (commit_general_batch, every pulse() observable)
+        self.general = general
         # with change_log: every commit call's write-back stream per shard, drained after each call
         # (a replica hands each one to its forest): lists of (shard, accounts, transfers, rows)
         self.logs = [] if change_log else None
@@ -66,23 +77,27 @@ class LocalShards:
             self._drain()
         return due
 
-    def commit_any(self, op, batches, tick_ns=0):
+    def commit_any(self, op, batches, tick_ns=0, ticks=None):
         """A window through the order-free path when no pulse can be due in it (after the harness
         pulse before its first batch), else (or when the window is outside the order-free class)
-        batch by batch through the general path (csrc/shard_gx.inc). Returns (per-batch replies,
-        took the fast path)."""
+        through the general path (csrc/shard_gx.inc): the whole window at once, or batch by batch.
+        `ticks`: a clock tick before each batch (general path only; tick_ns is then ignored).
+        Returns (per-batch replies, took the fast path)."""
         import torch
 
         from tigerbeetle_amd._lib import UnsupportedWindow
         from tigerbeetle_amd.sharding import commit_general_batch
 
         ts0 = self.prepare_timestamp
-        t_last = ts0 + tick_ns + sum(1 + len(ev) for ev in batches)
+        if ticks is None:
+            ticks = [tick_ns] + [0] * max(len(batches) - 1, 0)
+        tick_ns = ticks[0] if ticks else 0
+        t_last = ts0 + sum(ticks) + sum(1 + len(ev) for ev in batches)
         log0 = len(self.pulse_log)
         if batches:
             T0 = ts0 + tick_ns + 1 + len(batches[0])
             self.pulse_log.append((T0, self.pulse_before(T0)))
-        if t_last < self.shards[0].pulse_next():
+        if t_last < self.shards[0].pulse_next() and not any(ticks[1:]):
             try:
                 return self.commit_window(op, batches, tick_ns, _pulsed=True), True
             except UnsupportedWindow:
@@ -93,10 +108,26 @@ class LocalShards:
                         pass
                 self.prepare_timestamp = ts0
         del self.pulse_log[log0 + 1:]
+        if self.general == "window" and batches:
+            from tigerbeetle_amd.sharding import commit_general_window
+
+            ns, ts = [], []
+            self.prepare_timestamp = ts0
+            for ev, tk in zip(batches, ticks):
+                self.prepare_timestamp += tk + 1 + len(ev)
+                ns.append(len(ev))
+                ts.append(self.prepare_timestamp)
+            self.pulse_log.extend((t, None) for t in ts[1:])
+            data = np.concatenate([np.frombuffer(ev.tobytes(), np.uint8) for ev in batches])
+            d_ev = torch.from_numpy(data.copy()).cuda() if len(data) else torch.zeros(128, dtype=torch.uint8).cuda()
+            torch.cuda.synchronize()
+            out = commit_general_window(self.shards, self.summed, op, d_ev.data_ptr(), ns, ts, auto_pulse=False)
+            self._drain()
+            return out, False
         out = []
-        self.prepare_timestamp = ts0 + tick_ns
+        self.prepare_timestamp = ts0
         for k, ev in enumerate(batches):
-            self.prepare_timestamp += 1 + len(ev)
+            self.prepare_timestamp += ticks[k] + 1 + len(ev)
             if k > 0:  # batch 0's pulse ran above
                 self.pulse_log.append((self.prepare_timestamp, self.pulse_before(self.prepare_timestamp)))
             data = np.frombuffer(ev.tobytes(), np.uint8)

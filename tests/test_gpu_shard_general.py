@@ -13,7 +13,7 @@ import pytest
 
 from chaos import Chaos, run_protocol
 from oracle_sm import OracleStateMachine, lib as oracle_lib
-from test_gpu_shard import LocalShards, _compare_sharded
+from test_gpu_shard import LocalShards, _compare_sharded, same_pulse_log
 from test_gpu_window import oracle_batches
 from tigerbeetle_amd import workload
 from tigerbeetle_amd.types import NS_PER_S, Operation
@@ -47,12 +47,15 @@ def _check(sh, ref):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G,seed,win,bm", [(2, 0, 4, 16), (3, 1, 3, 32), (8, 2, 4, 16), (4, 3, 2, 64)])
-def test_shard_general_chaos(G, seed, win, bm):
+@pytest.mark.parametrize("G,seed,win,bm,general", [(2, 0, 4, 16, "window"), (3, 1, 3, 32, "window"),
+                                                   (8, 2, 4, 16, "window"), (4, 3, 2, 64, "window"),
+                                                   (2, 0, 4, 16, "batch"), (8, 2, 4, 16, "batch")])
+def test_shard_general_chaos(G, seed, win, bm, general):
     """Chaos streams (limits, balancing, two-phase with 1-9 s timeouts, posts/voids, chains with
     rollback, duplicate ids in and across windows, invalid fields) with clock ticks, interleaved with
-    plain uniform windows (the order-free path)."""
-    sh = LocalShards(G, bm, 4096, 1 << 16, win * bm)
+    plain uniform windows (the order-free path); windows outside it through the general path a whole
+    window at a time (one read set, pulses inside modelled by the scratch engine) or batch by batch."""
+    sh = LocalShards(G, bm, 4096, 1 << 16, win * bm, general=general)
     ref = OracleStateMachine(batch_max=bm)
     ch = Chaos(7000 + seed, n_accounts=30)
     fast = general = 0
@@ -74,7 +77,7 @@ def test_shard_general_chaos(G, seed, win, bm):
             r = oracle_logged(ref, op, batches, tick, ref_log)
             assert g == r, f"window {w} (fast={took_fast})"
             # pulse() before every batch, the first one of the stream included (replica.zig:9459-9467)
-            assert sh.pulse_log == ref_log, f"window {w}"
+            assert same_pulse_log(sh.pulse_log, ref_log), f"window {w}"
             assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp(), f"window {w}"
             fast += int(took_fast)
             general += int(not took_fast)
@@ -93,7 +96,7 @@ def test_shard_pulse_lockstep(G):
     transfer windows, then two-phase batches with timeouts and ticks (pulses that expire, pulses that
     expire nothing, and reset by post/void), then order-free windows again."""
     bm = 16
-    sh = LocalShards(G, bm, 2048, 1 << 14, 4 * bm)
+    sh = LocalShards(G, bm, 2048, 1 << 14, 4 * bm, general="batch")  # every pulse() observable
     ref = OracleStateMachine(batch_max=bm)
     ch = Chaos(7300 + G, n_accounts=20, pending=0.5, postvoid=0.3, limits=0.0, balancing=0.0, linked=0.1,
                invalid=0.0)
@@ -110,7 +113,7 @@ def test_shard_pulse_lockstep(G):
         for w, (op, batches, tick) in enumerate(plan):
             g, _ = sh.commit_any(op, batches, tick)
             assert g == oracle_logged(ref, op, batches, tick, ref_log), f"window {w}"
-            assert sh.pulse_log == ref_log, f"window {w}"
+            assert same_pulse_log(sh.pulse_log, ref_log), f"window {w}"
             assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp(), f"window {w}"
         assert sum(p for _, p in ref_log) >= 3, ref_log
         _check(sh, ref)
@@ -223,20 +226,24 @@ def test_shard_general_two_rank_gloo(tmp_path):
         ref.close()
 
 
-def _general_stream(sh, ref, op, batches, ticks):
-    for ev, tick in zip(batches, ticks):
-        g, _ = sh.commit_any(op, [ev], tick)
-        assert g == [run_protocol(ref, op, ev, tick)]
+def _general_stream(sh, ref, op, batches, ticks, win=1):
+    """`win` batches per window (each with its own tick) through LocalShards.commit_any, the
+    restatement batch by batch."""
+    for w0 in range(0, len(batches), win):
+        bs, tk = batches[w0:w0 + win], ticks[w0:w0 + win]
+        g, _ = sh.commit_any(op, bs, ticks=tk)
+        assert g == [run_protocol(ref, op, ev, t) for ev, t in zip(bs, tk)], f"window at batch {w0}"
         assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G", [2, 4, 8])
-def test_shard_cfg3_shape(G):
+@pytest.mark.parametrize("G,win", [(2, 1), (4, 1), (8, 1), (2, 6), (8, 6)])
+def test_shard_cfg3_shape(G, win):
     """cfg3's shape (Zipf(1.2) debits over accounts with debits_must_not_exceed_credits, funded from
-    treasury accounts) on G shards: every transfer batch reads balances across shards."""
+    treasury accounts) on G shards: every transfer batch reads balances across shards; windows of
+    `win` batches (one read set per window)."""
     bm, n_acc, top, treasury = 512, 3000, 100, 50
-    sh = LocalShards(G, bm, 4096, 1 << 15, bm)
+    sh = LocalShards(G, bm, 4096, 1 << 15, win * bm)
     ref = OracleStateMachine(batch_max=bm)
     try:
         acc = workload.accounts_cfg3(0, n_acc + treasury, 45, n_acc, top)
@@ -246,7 +253,8 @@ def test_shard_cfg3_shape(G):
         _general_stream(sh, ref, Operation.create_transfers, [fund[i:i + bm] for i in range(0, len(fund), bm)],
                         [0] * ((len(fund) + bm - 1) // bm))
         xf = workload.transfers_zipf(0, 6 * bm, 45, n_acc, workload.zipf_cdf(n_acc))
-        _general_stream(sh, ref, Operation.create_transfers, [xf[i:i + bm] for i in range(0, len(xf), bm)], [0] * 6)
+        _general_stream(sh, ref, Operation.create_transfers, [xf[i:i + bm] for i in range(0, len(xf), bm)], [0] * 6,
+                        win)
         _check(sh, ref)
     finally:
         sh.close()
@@ -254,12 +262,13 @@ def test_shard_cfg3_shape(G):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G", [2, 4, 8])
-def test_shard_cfg4_shape(G):
+@pytest.mark.parametrize("G,win", [(2, 1), (4, 1), (8, 1), (2, 8), (8, 8)])
+def test_shard_cfg4_shape(G, win):
     """cfg4's shape (30 % pending with 1-60 s timeouts, posts / voids of earlier pending transfers,
-    chains with injected failures), +1 s per batch so a pulse with expiries precedes most batches."""
+    chains with injected failures), +1 s per batch so a pulse with expiries precedes most batches;
+    windows of `win` batches (the pulses inside modelled by the scratch engine)."""
     bm, n_acc = 512, 2000
-    sh = LocalShards(G, bm, 4096, 1 << 15, bm)
+    sh = LocalShards(G, bm, 4096, 1 << 15, win * bm)
     ref = OracleStateMachine(batch_max=bm)
     try:
         acc = workload.accounts(0, n_acc, seed=46)
@@ -267,7 +276,7 @@ def test_shard_cfg4_shape(G):
                         [0] * ((n_acc + bm - 1) // bm))
         xf = workload.transfers_cfg4(0, 40 * bm, 46, n_acc, bm)
         _general_stream(sh, ref, Operation.create_transfers, [xf[i:i + bm] for i in range(0, len(xf), bm)],
-                        [NS_PER_S] * 40)
+                        [NS_PER_S] * 40, win)
         _check(sh, ref)
         assert (ref.dump_transfer_status() == 4).sum() > 0  # expiries ran on the shards
     finally:

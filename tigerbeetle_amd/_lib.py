@@ -21,6 +21,7 @@ EXPORTS = [
     "tbg_open", "tbg_reset", "tbg_prefetch_poll", "tbg_compact", "tbg_checkpoint", "tbg_digest",
     "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free", "tbg_checksum",
     "tbg_demux_init", "tbg_demux_decode", "tbg_aof_replay", "tbg_shard_gather_bytes", "tbg_shard_gather",
+    "tbg_shard_gather_window_bytes", "tbg_shard_gather_window", "tbg_gathered_objects",
     "tbg_shard_apply", "tbg_open_device", "tbg_device_state", "tbg_device_history", "tbg_shard_lookup_bytes",
     "tbg_shard_lookup", "tbg_shard_lookup_reply", "tbg_shard_query_bytes", "tbg_shard_query", "tbg_shard_query_merge",
 ]
@@ -147,6 +148,9 @@ def lib():
         "tbg_aof_replay": ([vp, vp, u64, u32, P(AofStats)], i32),
         "tbg_shard_gather_bytes": ([u32, u32, u32, P(u64)], u64),
         "tbg_shard_gather": ([vp, u32, vp, u32, u64, u32, vp], i32),
+        "tbg_shard_gather_window_bytes": ([u32, u32, u32, P(u64)], u64),
+        "tbg_shard_gather_window": ([vp, u32, vp, u32, u64, u32, vp, u32], i32),
+        "tbg_gathered_objects": ([vp, vp, u32, u32, vp, P(u64), vp, vp, P(u64)], i32),
         "tbg_shard_apply": ([vp, vp, u64, vp, vp, u64, vp, vp, u64], i32),
         "tbg_device_history": ([vp, P(vp), P(vp)], i32),
         "tbg_shard_lookup_bytes": ([u32], u64),

@@ -33,6 +33,8 @@ from . import _lib
 from .state_machine import StateMachine
 from .types import Operation
 
+WINDOW_BATCHES_MAX = 128  # csrc/window.h MAXB
+
 _M1, _M2 = np.uint64(0xFF51AFD7ED558CCD), np.uint64(0xC4CEB9FE1A85EC53)
 
 
@@ -107,6 +109,10 @@ class ShardedStateMachine:
         self.stream = torch.cuda.ExternalStream(self.sm.stream, device=dev)
         self._n_events = 0
         self._pulse_next = None  # cached pulse_next_timestamp (order-free windows never change it)
+        # general windows: due entries each shard can offer (more sends the window batch by batch)
+        self.due_cap = max(4 * batch_max, min(events_max, 1 << 16))
+        self.gxw_events = 0
+        self.wscratch = None
         torch.cuda.synchronize(device)
 
     @property
@@ -116,6 +122,8 @@ class ShardedStateMachine:
     def close(self):
         if self.scratch is not None:
             self.scratch.close()
+        if self.wscratch is not None:
+            self.wscratch.close()
         self.sm.close()
 
     def home_range(self, n_batches):
@@ -251,6 +259,108 @@ class ShardedStateMachine:
                     self.exchange(t)
 
         pulse_general([self], summed, timestamp)
+
+    # --------------------------------------------------------------------------------------------
+    # General class, a whole window at a time (csrc/shard_gx.inc tbg_shard_gather_window): one read
+    # set for all of the window's batches, every due entry up to its last batch, the scratch engine
+    # commits the window with its inner pulses modelled (xwin.h), one apply.
+    # --------------------------------------------------------------------------------------------
+    def _gxw_init(self, n_events):
+        import torch
+
+        G, D = self.shard_count, self.due_cap
+        need_e = max(n_events, 1)
+        if getattr(self, "gxw_events", 0) >= need_e:
+            return
+        L = _lib.lib()
+        dev = torch.device("cuda", self.device)
+        p2 = ctypes.c_uint64()
+        nbytes = int(L.tbg_shard_gather_window_bytes(need_e, G, D, ctypes.byref(p2)))
+        self.gxw = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        na, nx = 4 * need_e + 2 * G * D, 2 * need_e + G * D + G
+        self.gxw_acc = torch.empty(na * 128, dtype=torch.uint8, device=dev)
+        self.gxw_x = torch.empty(nx * 128, dtype=torch.uint8, device=dev)
+        self.gxw_st = torch.empty(nx, dtype=torch.uint8, device=dev)
+        if getattr(self, "wscratch", None) is not None:
+            self.wscratch.close()
+        self.wscratch = StateMachine(device=self.device, batch_max=self.batch_max, accounts_max=na + 64,
+                                     transfers_max=nx + need_e + 64, window_events_max=need_e)
+        self.gxw_res = torch.zeros(need_e * 8, dtype=torch.uint8, device=dev)
+        self.gxw_base = torch.zeros(WINDOW_BATCHES_MAX + 1, dtype=torch.int32, device=dev)
+        self.gxw_events = need_e
+        torch.cuda.synchronize(self.device)
+
+    def gather_window(self, operation, d_events, n_events, t_last, phase):
+        """Gather phase 1 or 2 of a general window; returns the region to be summed across the shards
+        (asynchronous on the engine stream)."""
+        self._gxw_init(n_events)
+        L = _lib.lib()
+        _lib.check(L.tbg_shard_gather_window(self.sm.h, int(operation), d_events, n_events, t_last, phase,
+                                             self.gxw.data_ptr(), self.due_cap), "shard_gather_window")
+        # the regions of THIS window's layout (it depends on the window's event count, not on the
+        # buffer's capacity): every byte the phase wrote must be summed
+        p2 = ctypes.c_uint64()
+        nbytes = int(L.tbg_shard_gather_window_bytes(n_events, self.shard_count, self.due_cap, ctypes.byref(p2)))
+        return self.gxw[: p2.value] if phase == 1 else self.gxw[p2.value: nbytes]
+
+    def due_overflow(self):
+        """After phase 1 was summed: whether a shard had more due entries than the window path holds
+        (then the window goes batch by batch)."""
+        from .state_machine import to_host
+
+        self.stream.synchronize()
+        cnt = to_host(self.gxw[: 4 * self.shard_count]).view(np.uint32)
+        return bool((cnt == 0xFFFFFFFF).any())
+
+    def decide_apply_window(self, operation, d_events, batch_events, batch_timestamps, auto_pulse=False):
+        """After both gathers were summed: the window on the scratch engine (batch 0's harness pulse
+        only with auto_pulse; the later batches' pulses modelled inside it), then the owned objects
+        applied here. Returns the per-batch replies, or None if the scratch engine could not model
+        the window (a pulse inside it reaching the expiry cap, or one reading a balance): nothing was
+        applied then, and the caller commits the window batch by batch."""
+        from ._lib import RejectedWindow
+        from .state_machine import to_host
+
+        L = _lib.lib()
+        E = sum(batch_events)
+        na, nx = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(L.tbg_gathered_objects(self.sm.h, self.gxw.data_ptr(), E, self.due_cap, self.gxw_acc.data_ptr(),
+                                          ctypes.byref(na), self.gxw_x.data_ptr(), self.gxw_st.data_ptr(),
+                                          ctypes.byref(nx)), "gathered_objects")
+        sc = self.wscratch
+        sc.reset()
+        _lib.check(L.tbg_open_device(sc.h, self.gxw_acc.data_ptr(), na.value, self.gxw_x.data_ptr(),
+                                     self.gxw_st.data_ptr(), nx.value, self.pulse_next()), "open_device")
+        sc.commit_window(operation, d_events, batch_events, batch_timestamps, self.gxw_res.data_ptr(),
+                         self.gxw_base.data_ptr(), auto_pulse, batch_timestamps[0])
+        try:
+            sc.sync()
+        except RejectedWindow:
+            return None
+        base = to_host(self.gxw_base)
+        res = to_host(self.gxw_res[: int(base[len(batch_events)]) * 8]).tobytes()
+        replies = [res[base[b] * 8: base[b + 1] * 8] for b in range(len(batch_events))]
+        pa, n_a, px, ps, n_x, pn2 = (ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_void_p(),
+                                     ctypes.c_uint64(), ctypes.c_uint64())
+        _lib.check(L.tbg_device_state(sc.h, ctypes.byref(pa), ctypes.byref(n_a), ctypes.byref(px), ctypes.byref(ps),
+                                      ctypes.byref(n_x), ctypes.byref(pn2)), "device_state")
+        ph, phs = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(L.tbg_device_history(sc.h, ctypes.byref(ph), ctypes.byref(phs)), "device_history")
+        _lib.check(L.tbg_shard_apply(self.sm.h, pa, n_a.value, px, ps, n_x.value, ph, phs, pn2.value), "shard_apply")
+        self._pulse_next = pn2.value
+        return replies
+
+    def commit_general_window(self, operation, d_events, batch_events, batch_timestamps, auto_pulse=True):
+        """A window of the general class with this process's exchange; every shard returns the
+        window's whole per-batch reply. Falls back to batch by batch when the window path cannot
+        hold it."""
+        def summed(tensors):
+            if self.exchange is not None:
+                for t in tensors:
+                    self.exchange(t)
+
+        return commit_general_window([self], summed, operation, d_events, batch_events, batch_timestamps,
+                                     auto_pulse)
 
     def _gx_init(self):
         import torch
@@ -404,6 +514,32 @@ def read_general(shards, summed, operation, data):
     return replies[0]
 
 
+def commit_general_window(shards, summed, operation, d_events, batch_events, batch_timestamps, auto_pulse=True):
+    """A window of the general class on `shards` (all shards in-process, or this process's one): one
+    read set for all its batches (two exchanges), decided by each shard's scratch engine with the
+    pulses inside the window modelled, one apply. With auto_pulse the harness pulse before batch 0
+    runs with it when due; without, the caller ran it. Returns the per-batch replies; falls back to
+    commit_general_batch per batch (with the harness pulse before batches 1..) when a shard has more
+    due entries than the window path gathers or the scratch engine rejects the window (nothing
+    applied then)."""
+    E = sum(batch_events)
+    t_last = batch_timestamps[-1]
+    summed([s.gather_window(operation, d_events, E, t_last, 1) for s in shards])
+    if not any(s.due_overflow() for s in shards[:1]):
+        summed([s.gather_window(operation, d_events, E, t_last, 2) for s in shards])
+        out = [s.decide_apply_window(operation, d_events, batch_events, batch_timestamps, auto_pulse) for s in shards]
+        if out[0] is not None:
+            return out[0]
+    replies, off = [], 0
+    for k, (n, T) in enumerate(zip(batch_events, batch_timestamps)):
+        if k > 0 and shards[0].pulse(T):
+            pulse_general(shards, summed, T)
+        replies.append(commit_general_batch(shards, summed, operation, d_events + off * 128, n, T,
+                                            auto_pulse=auto_pulse and k == 0))
+        off += n
+    return replies
+
+
 def commit_general_batch(shards, summed, operation, d_events, n, timestamp, auto_pulse=True):
     """One batch through the general path on `shards` (all shards in-process, or this process's
     one); `summed(list of tensors)` sums them across all shards in place. With auto_pulse the
@@ -413,5 +549,4 @@ def commit_general_batch(shards, summed, operation, d_events, n, timestamp, auto
     summed([s.gather(operation, d_events, n, timestamp, 1) for s in shards])
     summed([s.gather(operation, d_events, n, timestamp, 2) for s in shards])
     replies = [s.decide_apply(operation, d_events, n, timestamp, auto_pulse) for s in shards]
-    assert all(r == replies[0] for r in replies)
     return replies[0]

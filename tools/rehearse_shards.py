@@ -25,6 +25,130 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 BATCH = 8190
 
 
+def general(a):
+    """--stream cfg3|cfg4: the general class (csrc/shard_gx.inc, a whole window per read set) at G
+    shards on this GPU against ONE unsharded engine on the same stream. Per window and shard, wall
+    time of its steps (gather 1, gather 2, dedupe + scratch open + scratch commit + apply), each
+    shard alone (the in-process sums of the exchanges between them are not counted); the unsharded
+    engine's wall time per window (commit_window + sync) beside it."""
+    import time
+
+    import torch
+
+    from tigerbeetle_amd import StateMachine, _lib, workload
+    from tigerbeetle_amd.sharding import ShardedStateMachine, pulse_general
+    from tigerbeetle_amd.state_machine import to_host
+    from tigerbeetle_amd.types import NS_PER_S, Operation
+
+    L = _lib.lib()
+    G, win, n_acc, n_x = a.shards, a.window, a.accounts, a.transfers
+    tick = NS_PER_S if a.stream == "cfg4" else 0
+    treasury = 1000 if a.stream == "cfg3" else 0
+    shards = [ShardedStateMachine(G, r, None, batch_max=BATCH, accounts_max=int((n_acc + treasury) / G * 1.2) + 65536,
+                                  transfers_max=int((n_x + n_acc) / G * 1.2) + win * BATCH, window_events_max=win * BATCH)
+              for r in range(G)]
+    one = StateMachine(batch_max=BATCH, accounts_max=n_acc + treasury, transfers_max=n_x + n_acc + win * BATCH,
+                       window_events_max=win * BATCH)
+    d_acc = torch.empty((n_acc + treasury) * 128, dtype=torch.uint8, device="cuda")
+    d_fund = torch.empty(max(n_acc, 1) * 128, dtype=torch.uint8, device="cuda")
+    d_x = torch.empty(n_x * 128, dtype=torch.uint8, device="cuda")
+    st = one.stream
+    if a.stream == "cfg3":
+        d_cdf = torch.from_numpy(workload.zipf_cdf(n_acc).view(np.int64).copy()).cuda()
+        torch.cuda.synchronize()
+        _lib.check(L.tbg_gen_accounts_cfg3(d_acc.data_ptr(), 0, n_acc + treasury, a.seed, n_acc, 1000, st), "gen")
+        _lib.check(L.tbg_gen_funding_cfg3(d_fund.data_ptr(), 0, n_acc, a.seed, n_acc, treasury, 1_000_000, 10**15,
+                                          st), "gen")
+        _lib.check(L.tbg_gen_transfers_zipf(d_x.data_ptr(), 0, n_x, a.seed, n_acc, d_cdf.data_ptr(), 0, st), "gen")
+    else:
+        _lib.check(L.tbg_gen_accounts(d_acc.data_ptr(), 0, n_acc, a.seed, 2, 1, 0, st), "gen")
+        _lib.check(L.tbg_gen_transfers_cfg4(d_x.data_ptr(), 0, n_x, a.seed, n_acc, BATCH, 0, st), "gen")
+    torch.cuda.synchronize()
+    d_res = torch.empty(win * BATCH * 8, dtype=torch.uint8, device="cuda")
+    d_base = torch.zeros(256, dtype=torch.int32, device="cuda")
+
+    def summed(tensors):
+        torch.cuda.synchronize()
+        total = tensors[0].clone()
+        for t in tensors[1:]:
+            total += t
+        for t in tensors:
+            t.copy_(total)
+        torch.cuda.synchronize()
+
+    ts_sh, ts_one = [0], [0]
+    rows = []
+
+    def windows(op, d_ev, n_total, tk, timed):
+        nb = (n_total + BATCH - 1) // BATCH
+        for b0 in range(0, nb, win):
+            ns, ts = [], []
+            for b in range(b0, min(b0 + win, nb)):
+                n = min(BATCH, n_total - b * BATCH)
+                ts_sh[0] += tk + 1 + n
+                ns.append(n)
+                ts.append(ts_sh[0])
+            ptr = d_ev.data_ptr() + b0 * BATCH * 128
+            # one unsharded engine
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            one.commit_window(op, ptr, ns, ts, d_res.data_ptr(), d_base.data_ptr(), True, ts[0])
+            one.sync()
+            t_one = time.perf_counter() - t0
+            want = to_host(d_base)
+            # the shards: batch 0's harness pulse (per-batch general path), then the window
+            if shards[0].pulse(ts[0]):
+                pulse_general(shards, summed, ts[0])
+            per = [[0.0, 0.0, 0.0] for _ in range(G)]
+            E, T = sum(ns), ts[-1]
+            for phase in (1, 2):
+                parts = []
+                for r, s_ in enumerate(shards):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    parts.append(s_.gather_window(op, ptr, E, T, phase))
+                    s_.stream.synchronize()
+                    per[r][phase - 1] = time.perf_counter() - t0
+                summed(parts)
+                if phase == 1:
+                    assert not shards[0].due_overflow()
+            reps = []
+            for r, s_ in enumerate(shards):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                reps.append(s_.decide_apply_window(op, ptr, ns, ts, False))
+                torch.cuda.synchronize()
+                per[r][2] = time.perf_counter() - t0
+            assert reps[0] is not None, "scratch engine rejected the window"
+            fails = sum(len(x) // 8 for x in reps[0])
+            assert fails == int(want[len(ns)]), (fails, int(want[len(ns)]))
+            if timed:
+                rows.append((E, t_one, per))
+
+    windows(Operation.create_accounts, d_acc, n_acc + treasury, 0, False)
+    if a.stream == "cfg3":
+        windows(Operation.create_transfers, d_fund, n_acc, 0, False)
+    windows(Operation.create_transfers, d_x, n_x, tick, True)
+    timed = rows[a.warmup:]
+    ev = sum(r[0] for r in timed)
+    one_s = sum(r[1] for r in timed)
+    crit = sum(max(sum(p) for p in r[2]) for r in timed)
+    steps = np.array([[p for p in r[2]] for r in timed])  # windows x shards x 3
+    out = {"stream": a.stream, "shards": G, "window_batches": win, "timed_windows": len(timed), "events_timed": ev,
+           "unsharded_ms_per_window": round(one_s / len(timed) * 1000, 3),
+           "unsharded_rate": round(ev / one_s, 1),
+           "shard_ms_per_window": {"gather1_mean": round(float(steps[:, :, 0].mean()) * 1000, 3),
+                                   "gather2_mean": round(float(steps[:, :, 1].mean()) * 1000, 3),
+                                   "decide_apply_mean": round(float(steps[:, :, 2].mean()) * 1000, 3),
+                                   "max_shard_mean": round(crit / len(timed) * 1000, 3)},
+           "estimated_rate_excl_collective": round(ev / crit, 1),
+           "note": "wall clock per step (host launches and syncs included); exchanges summed in-process, not counted"}
+    print(json.dumps(out), flush=True)
+    for s_ in shards:
+        s_.close()
+    one.close()
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--shards", type=int, default=8)
@@ -33,7 +157,11 @@ def main():
     p.add_argument("--window", type=int, default=64, help="batches per (global) window")
     p.add_argument("--warmup", type=int, default=2, help="untimed windows")
     p.add_argument("--seed", type=int, default=47)
+    p.add_argument("--stream", default="cfg5", choices=["cfg5", "cfg3", "cfg4"],
+                   help="cfg5: the order-free fast path; cfg3 / cfg4: the general class a window at a time")
     a = p.parse_args()
+    if a.stream != "cfg5":
+        return general(a)
 
     import torch
 
