@@ -317,6 +317,7 @@ def cpu_baseline(args, seed):
     stream, same harness protocol (pulse when due, then the batch); only the commit calls are
     timed. Setup (accounts, cfg3 funding) is untimed, as on the GPU. The process is
     pinned to one host core for the measurement (restored after)."""
+    host = host_cpu()  # (before pinning: the usable CPUs of the process)
     try:
         saved = os.sched_getaffinity(0)
         pinned = min(saved)
@@ -328,6 +329,7 @@ def cpu_baseline(args, seed):
     finally:
         if saved is not None:
             os.sched_setaffinity(0, saved)
+    line.update(host)
     line["pinned_cpu"] = pinned
     return line
 
@@ -377,7 +379,6 @@ def _cpu_baseline(args, seed):
         "sample": f"first {events} transfers of the same {args.config} stream (same accounts and setup), "
                   f"{spent:.1f} s of commit time on 1 pinned host core (oracle/tb_oracle.c, -O2 -march=x86-64-v2)",
     }
-    line.update(host_cpu())
     return line
 
 

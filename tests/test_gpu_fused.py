@@ -484,3 +484,52 @@ def test_fused_resumes_after_overflow_bound_passes_2_63():
     finally:
         gpu.close()
         ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["random", "reversed"])
+def test_fused_claim_mode_ids_that_do_not_rise(order):
+    """Ids that do not rise (the reference benchmark's random and reversed IdPermutation): the fused
+    pass runs in claim mode (one key-map claim per id that reaches the exists check, tagged apart from
+    the general path's epochs), records hashed. A window with an in-window duplicate id leaves the
+    class (the second claimant) and goes to the general path; retries of stored ids are exists codes;
+    a rising window after them commits with claims and switches back to the rising-id test."""
+    n_acc = 2000
+    gpu, ref = _engines(n_acc, 1 << 20)
+    code = workload.ID_ORDERS[order]
+    try:
+        _accounts(gpu, ref, n_acc)
+        first = 0
+
+        def win(seed=31):
+            nonlocal first
+            b = _window(first, n_acc, seed=seed)
+            first += WIN * BM
+            flat = workload.permute_ids(np.concatenate(b), code, 99)
+            # (the account ids stay: only the transfer ids are permuted)
+            flat["debit_account_id_lo"], flat["debit_account_id_hi"] = np.concatenate(b)["debit_account_id_lo"], 0
+            flat["credit_account_id_lo"], flat["credit_account_id_hi"] = np.concatenate(b)["credit_account_id_lo"], 0
+            return [flat[k * BM:(k + 1) * BM].copy() for k in range(WIN)]
+
+        for w in range(3):
+            _check(gpu, ref, win())
+        assert gpu.stats()["fused_windows"] == 3
+        dup = win()
+        dup[5]["id_lo"][7], dup[5]["id_hi"][7] = dup[1]["id_lo"][3], dup[1]["id_hi"][3]  # in-window duplicate
+        _check(gpu, ref, dup)
+        assert gpu.stats()["fused_windows"] == 3
+        retry = win()
+        old = dup[2][:100].copy()
+        old["amount_lo"][::3] += 1  # exists_with_different_amount for some
+        retry[4][:100] = old
+        for w in range(4):  # back-off, then fused again (retries included)
+            _check(gpu, ref, retry if w == 0 else win())
+        # rising sequential ids (below the stored random ones: hashed, no prefix extension)
+        _check(gpu, ref, _window(first + 10**7, n_acc, seed=33))
+        _check(gpu, ref, _window(first + 2 * 10**7, n_acc, seed=34))
+        st = gpu.stats()
+        assert st["fused_windows"] >= 5
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()

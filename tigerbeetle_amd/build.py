@@ -16,8 +16,10 @@ def build_lib(force=False):
     deps = [os.path.join(HERE, p) for p in SOURCES + HEADERS]
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
-    cmd = ["hipcc"] + FLAGS + ["-o", out] + [os.path.join(HERE, s) for s in SOURCES]
+    tmp = out + ".tmp"  # built aside, then renamed over the library (a reader never sees a partial file)
+    cmd = ["hipcc"] + FLAGS + ["-o", tmp] + [os.path.join(HERE, s) for s in SOURCES]
     subprocess.check_call(cmd, cwd=HERE)
+    os.replace(tmp, out)
     return out
 
 

@@ -148,6 +148,8 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t sh_mis;         // sharded: this shard's ledger-mismatch slots used this window (shard.h)
   uint32_t sh_unsup;       // sharded: a home event outside the class this window (k_sh_count -> trailer 2)
   uint64_t ovf_rescans;    // times ovf_bound was re-tightened to the accounts' largest balance sum (restore.h)
+  uint32_t fu_nonmono;     // the epoch of a fused window whose ids did not all rise (claim mode, fused.h)
+  uint32_t pad5;
 };
 
 // The fused pass (fused.h) committed this window: the general path's kernels return at once.

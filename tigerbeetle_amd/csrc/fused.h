@@ -57,17 +57,46 @@ struct FuEv {
   bool simple, reach;
 };
 
-// prev_id: the id of event i - 1 (i > 0).
+// Claim mode (windows whose ids are not known to rise: Globals::mono_prev = 0): the ids that reach
+// the exists check claim a key-map entry tagged FU_CLAIM | epoch (never a general-path epoch, so a
+// window that leaves the class and goes to the general path finds them stale); a second claimant of
+// the same id is an in-window duplicate (outside the class). Returns whether `id` was already claimed
+// by another event.
+#define FU_CLAIM 0x80000000u
+__device__ __forceinline__ bool fu_claim(BEntry* bm, uint32_t mask, const uint8_t* ev, tb_uint128_t id, uint32_t i,
+                                         uint32_t tag) {
+  uint32_t h = (uint32_t)hash_id(id.lo, id.hi) & mask;
+  for (;;) {
+    unsigned long long old = __hip_atomic_load(&bm[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if (bk_epoch(old) != tag) {
+        const unsigned long long prev = atomicCAS(&bm[h].key, old, ((unsigned long long)tag << 32) | i);
+        if (prev == old) return false;
+        old = prev;
+        continue;
+      }
+      const tb_uint128_t k = bkey(ev, bk_owner(old), 0);
+      if (k.lo != id.lo || k.hi != id.hi) break;  // another id: probe on
+      return bk_owner(old) != i;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+// prev_id: the id of event i - 1 (i > 0). claim: claim mode (bm, bmask, tag), else the ids must rise.
 __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id, const tb_transfer_t& t,
-                                          u128 x_id_max, uint64_t P, FuEv* o) {
+                                          u128 x_id_max, uint64_t P, FuEv* o, bool claim = false,
+                                          BEntry* bm = nullptr, uint32_t bmask = 0, const uint8_t* evb = nullptr,
+                                          uint32_t tag = 0) {
   const uint16_t f = t.flags;
   o->dr = o->cr = NONE32;
   o->amount = 0;
   o->id_key = 0;
   o->reach = false;
-  // claim-free: ids strictly increasing over the window, no post/void (k_ct_prep's test)
+  // no chain, no post/void; claim-free (ids strictly increasing over the window, k_ct_prep's test)
+  // unless in claim mode
   bool simple = !(f & TB_TRANSFER_LINKED) && !(f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
-  if (i > 0) simple = simple && U(t.id) > prev_id;
+  if (i > 0 && !claim) simple = simple && U(t.id) > prev_id;
   uint32_t code;
   if (t.timestamp != 0) {
     code = TB_CT_TIMESTAMP_MUST_BE_ZERO;  // :1251
@@ -104,6 +133,7 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
             if (((de.flags | ce.flags) & TB_ACCOUNT_HISTORY) || (de.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) ||
                 (ce.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) || t.amount.hi != 0 || t.amount.lo >= FU_AMOUNT_MAX)
               simple = false;
+            if (claim && fu_claim(bm, bmask, evb, t.id, i, tag)) simple = false;  // in-window duplicate
             uint32_t xs = mx ? x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id) : NONE32;
             if (xs == NONE32 && mx) xs = x_prefix_find(d.xr, P, t.id);
             // :1506-1507; a plain create with timeout 0 cannot overflow the timeout (:1543)
@@ -159,7 +189,7 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   __shared__ uint32_t lds[FU_T / 64];
   __shared__ unsigned long long ldsu[FU_T / 64];
   __shared__ u128 ldsm[FU_T / 64];
-  __shared__ uint32_t aborted_lds;
+  __shared__ uint32_t ldsn[FU_T / 64];
   Globals* g = d.g;
   if (WIN_REJECTED(g)) return;
   const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -182,19 +212,23 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   const u128 ovf = g->ovf_bound;
   // window-level condition: the balance fields stay below 2^64 (ovf + 2^20 x 2^43 < 2^64)
   const bool glob_ok = (uint64_t)(ovf >> 64) == 0 && (uint64_t)ovf < (1ull << 63) && !g->batch_huge;
+  // claim mode: the previous transfer window's ids did not rise (e.g. random ids): in-window
+  // duplicates are found by claims instead of by the rising-id test
+  const bool claim = g->mono_prev == 0;
   if (k == 0 && threadIdx.x == 0) {
     // what k_fu_final reads while its last block updates the store counts
     g->fu_epoch = epoch;
     g->fu_base = base;
-    // the window extends the sorted prefix (claim-free when simple; first id above every stored id)
+    // the window may extend the sorted prefix (first id above every stored id; its ids must rise
+    // too: Globals::fu_nonmono, k_fu_final)
     g->fu_prefix = (P == base && U(ev[0].id) > x_id_max) ? 1u : 0u;
   }
-  // Another block may flag the window at any time: one read per block, so that every wave and
-  // fs.applied[k] agree on whether this block applies its adds (k_fu_final undoes exactly those).
-  if (threadIdx.x == 0)
-    aborted_lds = __hip_atomic_load(&g->fu_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch ? 1u : 0u;
-  __syncthreads();
-  const bool aborted = aborted_lds != 0;
+  // Another block may flag the window at any time, so waves of this block can read fu_abort
+  // differently: each wave reads it once (wave-uniform), and the block applies its adds only if NO
+  // wave saw it set (folded into the block vote below), so every wave and fs.applied[k] agree on
+  // whether this block applies (k_fu_final undoes exactly those).
+  const bool aborted = __builtin_amdgcn_readfirstlane(
+                           __hip_atomic_load(&g->fu_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch ? 1 : 0) != 0;
 
   tb_transfer_t t;
   FuEv fe;
@@ -230,15 +264,18 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
     prev = ((u128)__shfl_up(t.id.hi, 1, 64) << 64) | __shfl_up(t.id.lo, 1, 64);
     if (lane == 0 && i > 0 && i < E) prev = U(ev[i - 1].id);
   }
+  bool nonmono = false;  // (claim mode: whether the ids rise after all, for the next window)
   if (i < E && !aborted) {
-    fu_decide(d, i, prev, t, x_id_max, P, &fe);
+    fu_decide(d, i, prev, t, x_id_max, P, &fe, claim, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev),
+              FU_CLAIM | epoch);
+    nonmono = i > 0 && !(U(t.id) > prev);
     t.timestamp = win_ts(w, win_batch(w, i), i);  // :1253 (the record as inserted)
   }
-  const bool blk_simple = __syncthreads_and(fe.simple) && glob_ok && !aborted;
+  const bool blk_simple = __syncthreads_and(fe.simple && !aborted) && glob_ok;
   if (threadIdx.x == 0) {
     fs.applied[k] = blk_simple ? 1 : 0;
     // (a later block that reads this skips its work; k_fu_final reads it after the launch)
-    if (!blk_simple && !aborted) __hip_atomic_store(&g->fu_abort, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!blk_simple) __hip_atomic_store(&g->fu_abort, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (!blk_simple) return;
   const bool ok = i < E && fe.code == TB_CT_OK;
@@ -266,14 +303,16 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   const uint32_t wbad = (uint32_t)__popcll(__ballot(bad));
   const unsigned long long wsum = wave_sum_u64(fe.reach ? fe.amount : 0ull);
   const u128 wmax = wave_max_u128(fe.reach ? fe.id_key : (u128)0);
+  const bool wnm = __ballot(nonmono) != 0;
   if (lane == 0) {
     lds[wave] = wbad;
     ldsu[wave] = wsum;
     ldsm[wave] = wmax;
+    ldsn[wave] = wnm ? 1u : 0u;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t nbad = 0;
+    uint32_t nbad = 0, nm = 0;
     unsigned long long bsum = 0;
     u128 bmax = 0;
 #pragma unroll
@@ -281,8 +320,11 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
       nbad += lds[q];
       bsum += ldsu[q];
       bmax = umax128(bmax, ldsm[q]);
+      nm |= ldsn[q];
     }
     fs.cnt[k] = nbad;
+    // (claim mode) this block's ids do not rise: the window is hashed, and the next one claims too
+    if (nm) __hip_atomic_store(&g->fu_nonmono, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     fs.pay[k] = bsum;
     fs.idmax[k] = bmax;
     if (nbad) {
@@ -331,6 +373,7 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
     }
     if (!fs.applied[k] || i >= E) return;
     FuEv fe;
+    // (no claims: the undo needs the codes, amounts and accounts only)
     fu_decide(d, i, i > 0 ? U(ev[i - 1].id) : (u128)0, ev[i], g->x_id_max, g->x_sorted, &fe);
     if (fe.code == TB_CT_OK) {
       (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.dr].debits_posted), 0ull - fe.amount);
@@ -339,7 +382,8 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
     return;
   }
   const uint64_t base = g->fu_base;
-  const bool prefix_win = g->fu_prefix != 0;
+  const bool mono = g->fu_nonmono != epoch;
+  const bool prefix_win = g->fu_prefix != 0 && mono;
   const unsigned long long bw = g->fu_bad;
   const uint32_t total_bad = (uint32_t)(bw >> 32) == epoch ? (uint32_t)bw : 0u;
   if (!total_bad && prefix_win && k != gridDim.x - 1) {
@@ -414,7 +458,7 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
       if (prefix_win) g->x_sorted = base + total_ins;
       g->x_count = base + total_ins;
       g->win_flags = 1u | (prefix_win ? 2u : 0u);
-      g->mono_prev = 1;
+      g->mono_prev = mono ? 1u : 0u;  // (a window outside claim mode only commits with rising ids)
       g->ovf_bound += (u128)sum;  // below 2^64 (glob_ok, FU_AMOUNT_MAX)
       if (mx > g->x_id_max) g->x_id_max = mx;
       g->windows_applied++;

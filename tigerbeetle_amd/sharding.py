@@ -318,25 +318,32 @@ class ShardedStateMachine:
         applied here. Returns the per-batch replies, or None if the scratch engine could not model
         the window (a pulse inside it reaching the expiry cap, or one reading a balance): nothing was
         applied then, and the caller commits the window batch by batch."""
+        import time
+
         from ._lib import RejectedWindow
         from .state_machine import to_host
 
         L = _lib.lib()
         E = sum(batch_events)
+        times = getattr(self, "gxw_times", None)  # (rehearsal) wall time of each step, synced
+        t0 = time.perf_counter()
         na, nx = ctypes.c_uint64(), ctypes.c_uint64()
         _lib.check(L.tbg_gathered_objects(self.sm.h, self.gxw.data_ptr(), E, self.due_cap, self.gxw_acc.data_ptr(),
                                           ctypes.byref(na), self.gxw_x.data_ptr(), self.gxw_st.data_ptr(),
                                           ctypes.byref(nx)), "gathered_objects")
+        t1 = time.perf_counter()
         sc = self.wscratch
         sc.reset()
         _lib.check(L.tbg_open_device(sc.h, self.gxw_acc.data_ptr(), na.value, self.gxw_x.data_ptr(),
                                      self.gxw_st.data_ptr(), nx.value, self.pulse_next()), "open_device")
+        t2 = time.perf_counter()
         sc.commit_window(operation, d_events, batch_events, batch_timestamps, self.gxw_res.data_ptr(),
                          self.gxw_base.data_ptr(), auto_pulse, batch_timestamps[0])
         try:
             sc.sync()
         except RejectedWindow:
             return None
+        t3 = time.perf_counter()
         base = to_host(self.gxw_base)
         res = to_host(self.gxw_res[: int(base[len(batch_events)]) * 8]).tobytes()
         replies = [res[base[b] * 8: base[b + 1] * 8] for b in range(len(batch_events))]
@@ -348,6 +355,9 @@ class ShardedStateMachine:
         _lib.check(L.tbg_device_history(sc.h, ctypes.byref(ph), ctypes.byref(phs)), "device_history")
         _lib.check(L.tbg_shard_apply(self.sm.h, pa, n_a.value, px, ps, n_x.value, ph, phs, pn2.value), "shard_apply")
         self._pulse_next = pn2.value
+        if times is not None:
+            self.stream.synchronize()
+            times.append((t1 - t0, t2 - t1, t3 - t2, time.perf_counter() - t3, na.value, nx.value))
         return replies
 
     def commit_general_window(self, operation, d_events, batch_events, batch_timestamps, auto_pulse=True):

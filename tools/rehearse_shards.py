@@ -47,6 +47,8 @@ def general(a):
     shards = [ShardedStateMachine(G, r, None, batch_max=BATCH, accounts_max=int((n_acc + treasury) / G * 1.2) + 65536,
                                   transfers_max=int((n_x + n_acc) / G * 1.2) + win * BATCH, window_events_max=win * BATCH)
               for r in range(G)]
+    for s_ in shards:
+        s_.gxw_times = []
     one = StateMachine(batch_max=BATCH, accounts_max=n_acc + treasury, transfers_max=n_x + n_acc + win * BATCH,
                        window_events_max=win * BATCH)
     d_acc = torch.empty((n_acc + treasury) * 128, dtype=torch.uint8, device="cuda")
@@ -143,6 +145,13 @@ def general(a):
                                    "max_shard_mean": round(crit / len(timed) * 1000, 3)},
            "estimated_rate_excl_collective": round(ev / crit, 1),
            "note": "wall clock per step (host launches and syncs included); exchanges summed in-process, not counted"}
+    tt = np.array([t for s_ in shards for t in s_.gxw_times[-len(timed):]])
+    out["decide_apply_split_ms"] = {"objects": round(float(tt[:, 0].mean()) * 1000, 3),
+                                    "reset_open": round(float(tt[:, 1].mean()) * 1000, 3),
+                                    "scratch_commit": round(float(tt[:, 2].mean()) * 1000, 3),
+                                    "apply": round(float(tt[:, 3].mean()) * 1000, 3),
+                                    "objects_accounts_mean": int(tt[:, 4].mean()),
+                                    "objects_transfers_mean": int(tt[:, 5].mean())}
     print(json.dumps(out), flush=True)
     for s_ in shards:
         s_.close()
