@@ -108,7 +108,7 @@ def pmc_traffic(config, kernel, events_per_launch):
     FETCH_SIZE and WRITE_SIZE passes over the same bench command), scaled to this run's events per
     launch. Returns (raw FETCH+WRITE bytes, bytes with FETCH doubled per the gfx950 streaming-read
     correction, source) or None."""
-    for rnd in ("r3", "r2", "r1"):  # the latest round's summary of this config
+    for rnd in ("r4", "r3", "r2", "r1"):  # the latest round's summary of this config
         path = os.path.join(ROOT, "profiles", rnd, "pmc_%s.json" % config)
         if os.path.exists(path):
             break

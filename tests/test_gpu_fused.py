@@ -533,3 +533,37 @@ def test_fused_claim_mode_ids_that_do_not_rise(order):
     finally:
         gpu.close()
         ref.close()
+
+
+@pytest.mark.gpu
+def test_sync_prefetch_commit_runs_the_fused_pass():
+    """The synchronous StateMachine calls (pulse() check, prefetch, commit per batch: a replica that
+    does not pipeline): order-free batches commit through the fused pass (the prefetch only stages
+    the request), batches outside the class (pending with timeouts, limits, chains) are replayed
+    through the general path inside the same commit; replies and stores equal the restatement's."""
+    from chaos import run_protocol
+
+    n_acc = 2000
+    gpu, ref = _engines(n_acc + 2, 1 << 19)
+    try:
+        _accounts(gpu, ref, n_acc + 2, flags={n_acc: 2})
+        first = 0
+        for b in range(24):
+            ev = workload.transfers_uniform(first, BM, seed=41, n_accounts=n_acc)
+            first += BM
+            if b % 6 == 2:
+                ev["flags"][::37] = 2
+                ev["timeout"][::37] = 1
+            elif b % 6 == 4:
+                ev["debit_account_id_lo"][5] = n_acc + 1
+            elif b % 6 == 5:
+                ev["flags"][10:14] = 1
+            tick = 2 * 10**9 if b % 6 == 3 else 0
+            assert run_protocol(gpu, Operation.create_transfers, ev, tick) == \
+                run_protocol(ref, Operation.create_transfers, ev, tick), b
+        assert gpu.stats()["fused_windows"] >= 8
+        assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
