@@ -79,7 +79,7 @@ PHASE_KERNELS = {
 WALKED_EVENT_BYTES = 128 + 2 * 32 + 128
 
 CONFIGS = {
-    "cfg1": dict(accounts=10_000, transfers=1_000_000, window=64, seed=42, tick=0),
+    "cfg1": dict(accounts=10_000, transfers=1_000_000, window=32, seed=42, tick=0),
     "cfg2": dict(accounts=1_000_000, transfers=100_000_000, window=128, seed=44, tick=0),
     "cfg3": dict(accounts=1_000_000, transfers=10_000_000, window=32, seed=45, tick=0),
     "cfg4": dict(accounts=1_000_000, transfers=10_000_000, window=128, seed=46, tick=NS_PER_S),

@@ -551,12 +551,15 @@ def test_sync_prefetch_commit_runs_the_fused_pass():
         for b in range(24):
             ev = workload.transfers_uniform(first, BM, seed=41, n_accounts=n_acc)
             first += BM
-            if b % 6 == 2:
+            # batches outside the class (pending with timeouts, a limit account, chains) in the first
+            # half only: each backs the speculation off for 2^fails batches (1 + 2 + 4 + 8 here), so
+            # most of the clean second half runs fused again
+            if b < 12 and b % 6 == 2:
                 ev["flags"][::37] = 2
                 ev["timeout"][::37] = 1
-            elif b % 6 == 4:
-                ev["debit_account_id_lo"][5] = n_acc + 1
-            elif b % 6 == 5:
+            elif b < 12 and b % 6 == 4:
+                ev["debit_account_id_lo"][5] = n_acc + 1  # the account with a limit flag
+            elif b < 12 and b % 6 == 5:
                 ev["flags"][10:14] = 1
             tick = 2 * 10**9 if b % 6 == 3 else 0
             assert run_protocol(gpu, Operation.create_transfers, ev, tick) == \

@@ -105,6 +105,7 @@ template <bool XFER>
 __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t* ev, WinDesc w, uint32_t epoch) {
   Globals* g = d.g;
   if (!cpw_active(g)) return;
+  __shared__ uint2 pcache[256 * WCACHE];
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j == 0) g->cpw_done = 1;
   const bool on = j < g->cc_count;
@@ -138,7 +139,10 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
     atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)st_sum);
   }
   if (!on) return;
+  uint2* mine = pcache + threadIdx.x * WCACHE;
+  for (int k = 0; k < WCACHE; k++) mine[k] = make_uint2(NONE32, 0);
   Walker wk;
+  wk.pcache = mine;
   wk.d = d;
   wk.s = s;
   wk.s.undo = s.undo + 5ull * start;
@@ -146,6 +150,7 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
   wk.w = &w;
   wk.epoch = epoch;
   wk.atomic_bal = true;
+  wk.rows = XFER;
   wk.small_bal = g->small_win != 0;  // k_prep_reduce
   wk.template run<XFER>(s.rval + start, len);
 }

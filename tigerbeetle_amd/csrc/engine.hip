@@ -428,6 +428,8 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     s.p_tslot[i] = p_tslot;
     s.id_ent[i] = id_ent;
     s.pid_ent[i] = pid_ent;
+    s.wrow[2 * i] = make_uint4(code, id_tslot, id_ent, pid_ent);
+    s.wrow[2 * i + 1] = make_uint4(dr_slot, cr_slot, p_tslot, b);
     s.amt[i] = amt;
     if (cls & C_POSTVOID) s.pamt[i] = pamt;  // read only for post/void events (k_final)
     s.ins[i] = 0;
@@ -553,8 +555,14 @@ __global__ void __launch_bounds__(256) k_claim_fix(Dev d, Scratch s, const tb_tr
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x) {
     const uint32_t cls = s.cls[i];
     if (!(cls & C_REACH)) continue;
-    s.id_ent[i] = bmap_claim(s.bmap, s.bmask, evb, ev[i].id, i, 0, epoch);
-    if (cls & C_POSTVOID) s.pid_ent[i] = bmap_claim(s.bmap, s.bmask, evb, ev[i].pending_id, i, 1, epoch);
+    const uint32_t ie = bmap_claim(s.bmap, s.bmask, evb, ev[i].id, i, 0, epoch);
+    s.id_ent[i] = ie;
+    s.wrow[2 * i].z = ie;
+    if (cls & C_POSTVOID) {
+      const uint32_t pe = bmap_claim(s.bmap, s.bmask, evb, ev[i].pending_id, i, 1, epoch);
+      s.pid_ent[i] = pe;
+      s.wrow[2 * i].w = pe;
+    }
   }
 }
 

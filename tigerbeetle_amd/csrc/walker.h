@@ -76,79 +76,13 @@ __device__ inline void bmap_set_committed(BEntry* bm, uint32_t e, uint32_t epoch
 }
 
 // An event's static inputs (written by k_ct_prep / k_classify before any walker runs, never by a
-// walker for a later event).
+// walker for a later event), loaded one event ahead so the walk pays only its dynamic reads.
 struct WPre {
   uint32_t i, cls, b, code, id_tslot, id_ent, dr, cr, p_tslot, pid_ent;
+  bool id_alone;  // no other event of the window carries this id: no earlier commit of it to look up
+  uint4 head;     // transfers: the event's first 16 B (its id), loaded one event ahead: the load brings
+                  // the record's line into the cache, so the rest of it is a cache hit when it runs
 };
-
-// Transfers (run_x) load the rest of an event's inputs ahead of its turn as well:
-//   WDyn, two turns ahead: the raw key-map commit words of its id and pending id, and its batch's
-//         bounds and commit timestamp. A commit made by a turn in between is forwarded (cf, pf).
-//   WRec, one turn ahead: its body and, for a post/void, the pending transfer's record, accounts and
-//         status (pc: the window event the record was read from; -1: none, or a stored one).
-// ok = false: a rollback (or, for WRec, a forwarded pending commit) left the loaded values stale;
-// the turn reloads them.
-#define FW_NONE (-2)
-struct WDyn {
-  unsigned long long cw, pw;
-  uint32_t off0, off1;
-  uint64_t T;
-  int32_t cf, pf;
-  bool ok;
-};
-#ifndef WALK_REC_REGS
-#define WALK_REC_REGS 1
-#endif
-struct WRec {
-#if WALK_REC_REGS
-  tb_transfer_t t;
-  uint4 pq[6];  // the pending record's 16 B words 1-3 and 5-7 (all but its id and pending_id, unused)
-#else
-  uint4 th, ph;  // the body's first and the pending record's second 16 B: their lines, ahead
-  const tb_transfer_t* pp;
-#endif
-  uint32_t drs, crs;
-  int32_t pc;
-  uint8_t pst;
-  bool ok;
-};
-__device__ __attribute__((always_inline)) inline void prec_load(uint4* pq, const tb_transfer_t* src) {
-  const uint4* q = reinterpret_cast<const uint4*>(src);
-  pq[0] = q[1];
-  pq[1] = q[2];
-  pq[2] = q[3];
-  pq[3] = q[5];
-  pq[4] = q[6];
-  pq[5] = q[7];
-}
-__device__ __attribute__((always_inline)) inline tb_transfer_t prec_view(const uint4* pq) {
-  tb_transfer_t p;
-  uint4* q = reinterpret_cast<uint4*>(&p);
-  q[0] = make_uint4(0, 0, 0, 0);
-  q[1] = pq[0];
-  q[2] = pq[1];
-  q[3] = pq[2];
-  q[4] = make_uint4(0, 0, 0, 0);
-  q[5] = pq[3];
-  q[6] = pq[4];
-  q[7] = pq[5];
-  return p;
-}
-// What a turn wrote that inputs already loaded for later turns may hold.
-struct WEff {
-  uint32_t cent;  // the key-map entry it committed (NONE32: none)
-  uint32_t bst;   // the window's pending transfer whose status it set (NONE32: none)
-  uint32_t xst;   // the stored pending transfer whose status it set (NONE32: none)
-  uint8_t v;      // the status it set
-};
-
-// In a window with pulses inside: whether a post/void in a batch committed at T_b finds pending
-// transfer p already expired by one of the window's pulses (xw_expired_before, batch time given).
-__device__ inline bool xw_expired_at(const WinDesc& w, const tb_transfer_t& p, uint64_t T_b) {
-  if (!w.xwin || p.timeout == 0) return false;
-  const uint64_t exp = expires_at_of(p);
-  return xw_visible(p.timestamp, exp) && exp <= T_b;
-}
 
 struct Walker {
   Dev d;
@@ -167,11 +101,18 @@ struct Walker {
   // balance delta is a no-return 64-bit add on the low word (mod 2^64; the true value never leaves
   // the low word) and no walker waits for an atomic's result.
   bool small_bal = false;
-  // pulse_next as the window's pulse left it (walkers never change it: k_final and k_xwin_replay run
-  // after them) and whether win_flags bit 3 is known to be set: read once per walk instead of on
-  // every post/void of a timed pending transfer created in the window.
-  uint64_t pn0 = 0;
-  bool wf8 = false;
+  // This walker's recent commits (id key-map entry -> event index), direct-mapped in LDS: a
+  // post/void of a pending transfer its component created finds it without the key-map read (a
+  // component's keys are committed by its own walker only; cleared on every rollback). nullptr: off.
+  uint2* pcache = nullptr;
+  // create_transfers component walkers: an event's static inputs from its Scratch::wrow row
+  bool rows = false;
+#define WCACHE 8
+  __device__ __attribute__((always_inline)) int32_t pcache_find(uint32_t ent) const {
+    if (!pcache) return -1;
+    const uint2 c = pcache[ent & (WCACHE - 1)];
+    return c.x == ent ? (int32_t)c.y : -1;
+  }
 
   __device__ __attribute__((always_inline)) void log_bal(uint32_t slot) {
     if (!scope) return;
@@ -207,6 +148,8 @@ struct Walker {
     r.old[0] = v;
   }
   __device__ __attribute__((always_inline)) void rollback() {
+    if (pcache)
+      for (int k = 0; k < WCACHE; k++) pcache[k] = make_uint2(NONE32, 0);
     while (undo_n) {
       const UndoRec& r = s.undo[--undo_n];
       switch (r.kind) {
@@ -253,134 +196,72 @@ struct Walker {
     s.hside[i] = side;
   }
 
-  // Inserts event i's record t2 and commits its id (key-map entry e).
-  __device__ __attribute__((always_inline)) void commit_record(uint32_t i, uint32_t e, const tb_transfer_t& t2, WEff& f) {
+  __device__ __attribute__((always_inline)) void commit_record(uint32_t i, const tb_transfer_t& t2) {
     s.t2[i] = t2;
     s.hside[i] = 0;
     log_small(UNDO_INS, i, 0);
     s.ins[i] = 1;
+    const uint32_t e = s.id_ent[i];
     // (the entry had no commit this window, or the caller would have found it: undo restores
     // "none", epoch 0, without reading the old word)
     log_small(UNDO_COMMIT, e, 0);
     bmap_set_committed(s.bmap, e, epoch, (int32_t)i);
-    f.cent = e;
+    if (pcache) pcache[e & (WCACHE - 1)] = make_uint2(e, i);
   }
 
-  __device__ __attribute__((always_inline)) WPre pre(uint32_t i) const {
+  template <bool XFER>
+  __device__ __attribute__((always_inline)) WPre fetch(uint32_t i) {
     WPre e;
     e.i = i;
     e.cls = s.cls[i];
+    if (XFER && rows) {
+      const uint4 r0 = s.wrow[2 * i], r1 = s.wrow[2 * i + 1];
+      e.code = r0.x;
+      e.id_tslot = r0.y;
+      e.id_ent = r0.z;
+      e.pid_ent = r0.w;
+      e.dr = r1.x;
+      e.cr = r1.y;
+      e.p_tslot = r1.z;
+      e.b = r1.w;
+      e.head = reinterpret_cast<const uint4*>(ev)[(size_t)i * 8];
+      e.id_alone = (e.cls & C_IDALONE) != 0;
+      return e;
+    }
     e.b = s.batch[i];
     e.code = s.code[i];
     e.id_tslot = s.id_tslot[i];
     e.id_ent = s.id_ent[i];
-    e.dr = s.dr_slot[i];
-    e.cr = s.cr_slot[i];
-    e.p_tslot = s.p_tslot[i];
-    e.pid_ent = s.pid_ent[i];
+    if (XFER) {
+      e.dr = s.dr_slot[i];
+      e.cr = s.cr_slot[i];
+      e.p_tslot = s.p_tslot[i];
+      e.pid_ent = s.pid_ent[i];
+      e.head = reinterpret_cast<const uint4*>(ev)[(size_t)i * 8];
+    }
+    e.id_alone = (e.cls & C_IDALONE) != 0;  // k_classify
     return e;
-  }
-  // the key-map loads a turn may need (an entry exists only for events that reach the exists check)
-  __device__ static __attribute__((always_inline)) bool needs_c(const WPre& e) {
-    return (e.cls & (C_REACH | C_STATIC | C_IDALONE)) == C_REACH;
-  }
-  __device__ static __attribute__((always_inline)) bool needs_pc(const WPre& e) {
-    return (e.cls & (C_REACH | C_STATIC | C_POSTVOID)) == (C_REACH | C_POSTVOID) && e.p_tslot == NONE32;
-  }
-  __device__ __attribute__((always_inline)) WDyn dyn_x(const WPre& e) const {
-    WDyn y;
-    y.cw = y.pw = 0;
-    if (needs_c(e)) y.cw = s.bmap[e.id_ent].commit;
-    if (needs_pc(e)) y.pw = s.bmap[e.pid_ent].commit;
-    y.off0 = w->off[e.b];
-    y.off1 = w->off[e.b + 1];
-    y.T = w->T[e.b];
-    y.cf = y.pf = FW_NONE;
-    y.ok = true;
-    return y;
-  }
-  __device__ __attribute__((always_inline)) int32_t word_commit(unsigned long long c) const {
-    return bk_epoch(c) == epoch ? (int32_t)(uint32_t)c : -1;
-  }
-  __device__ __attribute__((always_inline)) int32_t dyn_c(const WPre& e, const WDyn& y) const {
-    if (y.cf != FW_NONE) return y.cf;
-    return needs_c(e) ? word_commit(y.cw) : -1;
-  }
-  __device__ __attribute__((always_inline)) int32_t dyn_pc(const WPre& e, const WDyn& y) const {
-    if (y.pf != FW_NONE) return y.pf;
-    return needs_pc(e) ? word_commit(y.pw) : -1;
-  }
-  __device__ __attribute__((always_inline)) WRec rec_x(const WPre& e, const WDyn& y) const {
-    WRec r;
-    r.ok = true;
-    r.pc = -1;
-    if (e.cls & C_STATIC) return r;
-#if WALK_REC_REGS
-    r.t = reinterpret_cast<const tb_transfer_t*>(ev)[e.i];
-#else
-    r.th = reinterpret_cast<const uint4*>(ev)[(size_t)e.i * 8];
-#endif
-    if (!(e.cls & C_POSTVOID)) return r;
-    const tb_transfer_t* pp = nullptr;
-    if (e.p_tslot != NONE32) {
-      pp = &d.xr[e.p_tslot];
-      r.drs = e.dr;
-      r.crs = e.cr;
-      r.pst = d.xstatus[e.p_tslot];
-    } else {
-      r.pc = dyn_pc(e, y);
-      if (r.pc >= 0) {
-        pp = &s.t2[r.pc];
-        r.drs = s.dr_slot[r.pc];
-        r.crs = s.cr_slot[r.pc];
-        r.pst = s.bstatus[r.pc];
-      }
-    }
-    if (pp) {
-#if WALK_REC_REGS
-      prec_load(r.pq, pp);
-#else
-      r.pp = pp;
-      r.ph = reinterpret_cast<const uint4*>(pp)[1];
-#endif
-    }
-    return r;
-  }
-  // A turn's writes into the inputs loaded for the next two turns (before those writes).
-  __device__ __attribute__((always_inline)) static void fwd(const WEff& f, int32_t ci, const WPre& e1, WDyn& y1,
-                                                            WRec& r1, const WPre& e2, WDyn& y2) {
-    if (f.cent != NONE32) {
-      if (needs_c(e1) && e1.id_ent == f.cent) y1.cf = ci;
-      if (needs_pc(e1) && e1.pid_ent == f.cent) {
-        y1.pf = ci;
-        r1.ok = false;
-      }
-      if (needs_c(e2) && e2.id_ent == f.cent) y2.cf = ci;
-      if (needs_pc(e2) && e2.pid_ent == f.cent) y2.pf = ci;
-    }
-    if (f.bst != NONE32 && r1.pc == (int32_t)f.bst) r1.pst = f.v;
-    if (f.xst != NONE32 && (e1.cls & C_POSTVOID) && e1.p_tslot == f.xst) r1.pst = f.v;
   }
 
   // create_transfer (:1462-1585) from the exists check on; validation results come from k_ct_prep.
-  __device__ __attribute__((always_inline)) uint32_t transfer(const WPre& e, const WDyn& y, const WRec& rc, WEff& f) {
+  __device__ __attribute__((always_inline)) uint32_t transfer(const WPre& e) {
     const uint32_t i = e.i;
     if (e.cls & C_STATIC) return e.code;
-    const int32_t c = dyn_c(e, y);
-#if WALK_REC_REGS
-    tb_transfer_t t = rc.t;
-#else
-    tb_transfer_t t;
-    {
-      const uint4* q = reinterpret_cast<const uint4*>(ev) + (size_t)i * 8;
-      uint4* tq = reinterpret_cast<uint4*>(&t);
-      tq[0] = rc.th;
-#pragma unroll
-      for (int k = 1; k < 8; k++) tq[k] = q[k];
+    // The key-map reads whose entries are known now (this event's id, a post/void's pending id) go
+    // out with the event body's load: a component's walk is a chain of dependent reads, and nothing
+    // this event does before their original use writes them.
+    const bool pv = e.cls & C_POSTVOID;
+    const int32_t c = e.id_alone ? -1 : bmap_committed(s.bmap, e.id_ent, epoch);
+    int32_t pc = -1;
+    if (pv && e.p_tslot == NONE32) {
+      pc = pcache_find(e.pid_ent);
+      if (pc < 0) pc = bmap_committed(s.bmap, e.pid_ent, epoch);
     }
-#endif
-    t.timestamp = y.T - (y.off1 - y.off0) + (i - y.off0) + 1;  // win_ts
-    if (e.cls & C_POSTVOID) return post_or_void(e, y, rc, t, c, f);
+    tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev)[i];
+    t.id.lo = ((uint64_t)e.head.y << 32) | e.head.x;
+    t.id.hi = ((uint64_t)e.head.w << 32) | e.head.z;
+    t.timestamp = win_ts(*w, e.b, i);
+    if (pv) return post_or_void(e, t, c, pc);
     if (e.id_tslot != NONE32) return ct_exists(t, d.xr[e.id_tslot]);
     if (c >= 0) return ct_exists(t, s.t2[c]);
     const uint32_t drs = e.dr, crs = e.cr;
@@ -402,7 +283,7 @@ struct Walker {
       if (r != TB_CT_OK) return r;
     }
     t.amount = W(amount);
-    commit_record(i, e.id_ent, t, f);
+    commit_record(i, t);
     if (atomic_bal) {
       const bool pend = t.flags & TB_TRANSFER_PENDING;
       add_bal(drs, pend ? 0 : 1, amount);
@@ -427,65 +308,64 @@ struct Walker {
   }
 
   // post_or_void_pending_transfer (:1608-1741) from the pending lookup on. `c`: this event's id
-  // committed earlier in the window (or -1); rc.pc: the in-window pending transfer (-1: none, or the
-  // pending transfer was stored before the window: p_tslot).
-  __device__ __attribute__((always_inline)) uint32_t post_or_void(const WPre& e, const WDyn& y, const WRec& rc,
-                                                                  const tb_transfer_t& t, int32_t c, WEff& f) {
+  // committed earlier in the window (or -1); `pc`: the in-window pending transfer (-1: none, or the
+  // pending transfer was stored before the window: p_tslot). The pending record, its accounts and its
+  // status are read together.
+  __device__ __attribute__((always_inline)) uint32_t post_or_void(const WPre& e, const tb_transfer_t& t, int32_t c,
+                                                                  int32_t pc) {
     const uint32_t i = e.i;
     const uint32_t pslot = e.p_tslot;
-    const int32_t pc = rc.pc;
-    if (pslot == NONE32 && pc < 0) return TB_CT_PENDING_TRANSFER_NOT_FOUND;
-#if WALK_REC_REGS
-    const tb_transfer_t p = prec_view(rc.pq);  // (its id and pending_id read as zero: not used below)
-#else
-    uint4 pq[6];
-    {
-      const uint4* q = reinterpret_cast<const uint4*>(rc.pp);
-      pq[0] = rc.ph;
-      pq[1] = q[2];
-      pq[2] = q[3];
-      pq[3] = q[5];
-      pq[4] = q[6];
-      pq[5] = q[7];
+    uint32_t drs, crs;
+    uint8_t pst0;
+    const tb_transfer_t* pp;  // one load from the selected record (no merged aggregate)
+    if (pslot != NONE32) {
+      pp = &d.xr[pslot];
+      drs = e.dr;
+      crs = e.cr;
+      pst0 = d.xstatus[pslot];
+    } else {
+      if (pc < 0) return TB_CT_PENDING_TRANSFER_NOT_FOUND;
+      pp = &s.t2[pc];
+      if (rows) {
+        const uint4 r1 = s.wrow[2 * pc + 1];
+        drs = r1.x;
+        crs = r1.y;
+      } else {
+        drs = s.dr_slot[pc];
+        crs = s.cr_slot[pc];
+      }
+      pst0 = s.bstatus[pc];
     }
-    const tb_transfer_t p = prec_view(pq);
-#endif
-    const uint32_t drs = rc.drs, crs = rc.crs;
+    const tb_transfer_t p = *pp;
     u128 amount;
     uint32_t r = pv_against(t, p, &amount);
     if (r != CONT) return r;
     if (e.id_tslot != NONE32) return pv_exists(t, d.xr[e.id_tslot], p);
     if (c >= 0) return pv_exists(t, s.t2[c], p);
-    uint8_t pst = rc.pst;
-    if (pst == TB_PENDING_PENDING && xw_expired_at(*w, p, y.T)) pst = TB_PENDING_EXPIRED;
+    uint8_t pst = pst0;
+    if (pst == TB_PENDING_PENDING && xw_expired_before(*w, p, s.batch[i])) pst = TB_PENDING_EXPIRED;
     r = pv_status(pst);
     if (r != CONT) return r;
-    commit_record(i, e.id_ent, pv_record(t, p, amount), f);
+    commit_record(i, pv_record(t, p, amount));
     if (p.timeout > 0 && expires_at_of(p) <= t.timestamp) return TB_CT_PENDING_TRANSFER_EXPIRED;
     if (pc >= 0 && p.timeout > 0) {
       // p was created in this window (k_ct_prep could not see it): the expires_at removal and the
       // pulse_next reset candidate (:1698-1708) for k_pn
-      const uint64_t pnv = expires_at_of(p);
-      s.pnv[i] = pnv;
+      s.pnv[i] = expires_at_of(p);
       s.pn_src[i] = (uint32_t)pc;
-      s.cls[i] = e.cls | C_PNOP;  // (no turn before this one wrote event i's class)
+      s.cls[i] |= C_PNOP;
       // may reset pulse_next (needs expires_at <= pulse_next as it was after the window's pulse,
       // which holds until k_final): k_final then replays the window's ops in order
-      if (pnv <= pn0 && !wf8) {
+      if (s.pnv[i] <= d.g->pulse_next && !(__hip_atomic_load(&d.g->win_flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8u))
         atomicOr(&d.g->win_flags, 8u);
-        wf8 = true;
-      }
     }
     const uint8_t st = (t.flags & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
-    f.v = st;
     if (pc >= 0) {
-      log_small(UNDO_BST, (uint32_t)pc, rc.pst);
+      log_small(UNDO_BST, (uint32_t)pc, pst0);
       s.bstatus[pc] = st;
-      f.bst = (uint32_t)pc;
     } else {
-      log_small(UNDO_XST, pslot, rc.pst);
+      log_small(UNDO_XST, pslot, pst0);
       d.xstatus[pslot] = st;
-      f.xst = pslot;
     }
     const u128 pa = U(p.amount);
     if (atomic_bal) {
@@ -529,133 +409,58 @@ struct Walker {
     return TB_CA_OK;
   }
 
-  // The chain bookkeeping of one turn (:1236-1300) around its outcome r; true: it rolled back.
-  __device__ __attribute__((always_inline)) bool settle(uint32_t i, uint32_t r, bool linked, int32_t& chain,
-                                                        bool& broken) {
-    bool rolled = false;
-    if (r != TB_CT_OK && chain >= 0 && !broken) {
-      broken = true;
-      rolled = undo_n != 0;
-      rollback();
-      for (uint32_t j = (uint32_t)chain; j < i; j++) {
-        s.code[j] = TB_CT_LINKED_EVENT_FAILED;
-        s.cls[j] |= C_RANOK;  // ran ok before the rollback: its pulse_next op stands (k_pn)
-      }
-    }
-    s.code[i] = r;
-    if (chain >= 0 && (!linked || r == TB_CT_LINKED_EVENT_CHAIN_OPEN)) {
-      chain = -1;
-      broken = false;
-      scope = false;
-      undo_n = 0;
-    }
-    return rolled;
-  }
-
-  // Transfers: the events list[0..count) (ascending window positions) as a four-stage software
-  // pipeline. An event's inputs load over the turns before its own: its list position (four turns
-  // ahead), its static inputs (three), its key-map commits and batch bounds (two), its body and its
-  // pending transfer's record and status (one). A turn then waits only for loads issued a turn
-  // earlier instead of a chain of dependent reads (a component's walk is one such chain per event);
-  // what a turn writes is forwarded into the inputs already loaded for the next two (fwd), and a
-  // rollback makes them reload.
-  __device__ void run_x(const uint32_t* list, uint32_t count) {
+  // Walks the events list[0..count) (ascending window positions).
+  template <bool XFER>
+  __device__ __attribute__((always_inline)) void run(const uint32_t* list, uint32_t count) {
     int32_t chain = -1;
     bool broken = false;
     undo_n = 0;
     scope = false;
-    pn0 = d.g->pulse_next;
-    wf8 = (__hip_atomic_load(&d.g->win_flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8u) != 0;
-    if (!count) return;
-    uint32_t i3 = count > 3 ? list[3] : 0u;
-    WPre e0 = pre(list[0]), e1, e2;
-    if (count > 1) e1 = pre(list[1]);
-    if (count > 2) e2 = pre(list[2]);
-    WDyn y0 = dyn_x(e0), y1;
-    if (count > 1) y1 = dyn_x(e1);
-    WRec r0 = rec_x(e0, y0);
+    // software pipeline: event k + 1's static inputs load while event k runs; list[k + 2] one
+    // step earlier still
+    WPre nx;
+    uint32_t i2 = NONE32;
+    if (count) nx = fetch<XFER>(list[0]);
+    if (count > 1) i2 = list[1];
     for (uint32_t k = 0; k < count; k++) {
-      WPre e3;
-      WDyn y2;
-      WRec r1;
-      uint32_t i4 = 0;
-      if (k + 3 < count) {
-        e3 = pre(i3);
-        if (k + 4 < count) i4 = list[k + 4];
+      const WPre cur = nx;
+      if (k + 1 < count) {
+        nx = fetch<XFER>(i2);
+        if (k + 2 < count) i2 = list[k + 2];
       }
-      if (k + 2 < count) y2 = dyn_x(e2);
-      if (k + 1 < count) r1 = rec_x(e1, y1);
-      if (!y0.ok) {
-        y0 = dyn_x(e0);
-        r0.ok = false;
-      }
-      if (!r0.ok) r0 = rec_x(e0, y0);
-      const uint32_t i = e0.i, cls = e0.cls;
+      const uint32_t i = cur.i;
+      const uint32_t cls = cur.cls;
       const bool linked = cls & C_LINKED;
-      WEff f = {NONE32, NONE32, NONE32, 0};
+      const uint32_t b = cur.b;
       uint32_t r;
       if (linked && chain < 0) {
         chain = (int32_t)i;
         undo_n = 0;
         scope = true;
       }
-      if (linked && i == y0.off1 - 1) {
+      if (linked && i == w->off[b + 1] - 1) {
         r = TB_CT_LINKED_EVENT_CHAIN_OPEN;
       } else if (broken) {
         r = TB_CT_LINKED_EVENT_FAILED;
       } else if (cls & C_TSNZ) {
         r = TB_CT_TIMESTAMP_MUST_BE_ZERO;
       } else {
-        r = transfer(e0, y0, r0, f);
+        r = XFER ? transfer(cur) : account(i, cls);
       }
-      if (settle(i, r, linked, chain, broken)) {
-        y1.ok = false;
-        r1.ok = false;
-        y2.ok = false;
-      } else {
-        fwd(f, (int32_t)i, e1, y1, r1, e2, y2);
+      if (r != TB_CT_OK && chain >= 0 && !broken) {
+        broken = true;
+        rollback();
+        for (uint32_t j = (uint32_t)chain; j < i; j++) {
+          s.code[j] = TB_CT_LINKED_EVENT_FAILED;
+          s.cls[j] |= C_RANOK;  // ran ok before the rollback: its pulse_next op stands (k_pn)
+        }
       }
-      e0 = e1;
-      e1 = e2;
-      e2 = e3;
-      i3 = i4;
-      y0 = y1;
-      y1 = y2;
-      r0 = r1;
-    }
-  }
-
-  // Walks the events list[0..count) (ascending window positions).
-  template <bool XFER>
-  __device__ __attribute__((always_inline)) void run(const uint32_t* list, uint32_t count) {
-    if constexpr (XFER) {
-      run_x(list, count);
-    } else {
-      int32_t chain = -1;
-      bool broken = false;
-      undo_n = 0;
-      scope = false;
-      for (uint32_t k = 0; k < count; k++) {
-        const uint32_t i = list[k];
-        const uint32_t cls = s.cls[i];
-        const bool linked = cls & C_LINKED;
-        const uint32_t b = s.batch[i];
-        uint32_t r;
-        if (linked && chain < 0) {
-          chain = (int32_t)i;
-          undo_n = 0;
-          scope = true;
-        }
-        if (linked && i == w->off[b + 1] - 1) {
-          r = TB_CT_LINKED_EVENT_CHAIN_OPEN;
-        } else if (broken) {
-          r = TB_CT_LINKED_EVENT_FAILED;
-        } else if (cls & C_TSNZ) {
-          r = TB_CT_TIMESTAMP_MUST_BE_ZERO;
-        } else {
-          r = account(i, cls);
-        }
-        settle(i, r, linked, chain, broken);
+      s.code[i] = r;
+      if (chain >= 0 && (!linked || r == TB_CT_LINKED_EVENT_CHAIN_OPEN)) {
+        chain = -1;
+        broken = false;
+        scope = false;
+        undo_n = 0;
       }
     }
   }

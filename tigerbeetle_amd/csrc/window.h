@@ -81,6 +81,10 @@ struct Dev {
 
 struct Scratch {
   uint32_t *code, *cls, *dr_slot, *cr_slot, *id_tslot, *p_tslot, *id_ent, *pid_ent, *wlist;
+  // create_transfers: the columns a walker reads per event, also as one 32 B row (k_ct_prep,
+  // k_claim_fix): {code, id_tslot, id_ent, pid_ent}, {dr_slot, cr_slot, p_tslot, batch}. A component
+  // walker reads each event's row with one request instead of eight column loads.
+  uint4* wrow;
   uint16_t* batch;
   uint8_t *ins, *bstatus;
   u128 *amt, *pamt;

@@ -200,6 +200,12 @@ class ShardedStateMachine:
         L = _lib.lib()
         op = int(operation)
         dev = torch.device("cuda", self.device)
+        with torch.cuda.stream(self.stream):  # the zero fill before the engine kernels that write into it
+            return self._read_request(L, op, dev, data)
+
+    def _read_request(self, L, op, dev, data):
+        import torch
+
         if op in (int(Operation.lookup_accounts), int(Operation.lookup_transfers)):
             buf = torch.zeros(max(int(L.tbg_shard_lookup_bytes(len(data) // 16)), 1), dtype=torch.uint8, device=dev)
             raw = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
@@ -230,8 +236,7 @@ class ShardedStateMachine:
     def read(self, operation, data):
         """lookup_* / get_account_* with this process's exchange: the reply bytes."""
         buf = self.read_request(operation, data)
-        if self.exchange is not None:
-            self.exchange(buf)
+        self._sum([buf])
         return self.read_reply(operation, data, buf)
 
     def window_changes(self):
@@ -249,16 +254,23 @@ class ShardedStateMachine:
         """StateMachine.pulse() (state_machine.zig:589-596): pulse_next_timestamp <= prepare_timestamp."""
         return self.pulse_next() <= prepare_timestamp
 
+    def _sum(self, tensors):
+        """This process's exchange over `tensors`, ordered on the engine stream: the tensors were
+        written by engine kernels still in flight (no sync after the gathers), and exchange_nccl /
+        exchange_gloo run on the current stream."""
+        import torch
+
+        if self.exchange is None:
+            return
+        with torch.cuda.stream(self.stream):
+            for t in tensors:
+                self.exchange(t)
+
     def commit_pulse(self, timestamp):
         """commit(.pulse) at `timestamp` with this process's exchange (the replica logs one when
         pulse() is true, vsr/replica.zig:9459-9487; the harness runs one before a batch at the
         batch's timestamp, :2719-2739)."""
-        def summed(tensors):
-            if self.exchange is not None:
-                for t in tensors:
-                    self.exchange(t)
-
-        pulse_general([self], summed, timestamp)
+        pulse_general([self], self._sum, timestamp)
 
     # --------------------------------------------------------------------------------------------
     # General class, a whole window at a time (csrc/shard_gx.inc tbg_shard_gather_window): one read
@@ -364,12 +376,7 @@ class ShardedStateMachine:
         """A window of the general class with this process's exchange; every shard returns the
         window's whole per-batch reply. Falls back to batch by batch when the window path cannot
         hold it."""
-        def summed(tensors):
-            if self.exchange is not None:
-                for t in tensors:
-                    self.exchange(t)
-
-        return commit_general_window([self], summed, operation, d_events, batch_events, batch_timestamps,
+        return commit_general_window([self], self._sum, operation, d_events, batch_events, batch_timestamps,
                                      auto_pulse)
 
     def _gx_init(self):
@@ -385,6 +392,7 @@ class ShardedStateMachine:
                                     transfers_max=3 * bm + G * C + G + 64, window_events_max=bm)
         self.gx_res = torch.zeros(max(bm, 1) * 8, dtype=torch.uint8, device=dev)
         self.gx_base = torch.zeros(2, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(self.device)  # (the fills ran on the current stream; the engine's next)
 
     def gather(self, operation, d_events, n, timestamp, phase):
         """Gather phase 1 or 2 of one batch; returns the region to be summed across the shards."""
@@ -400,12 +408,7 @@ class ShardedStateMachine:
     def commit_general(self, operation, d_events, n, timestamp):
         """One batch (its harness pulse included) through the general path with this process's
         exchange; every shard returns the batch's whole reply."""
-        def summed(tensors):
-            if self.exchange is not None:
-                for t in tensors:
-                    self.exchange(t)
-
-        return commit_general_batch([self], summed, operation, d_events, n, timestamp)
+        return commit_general_batch([self], self._sum, operation, d_events, n, timestamp)
 
     def decide_apply(self, operation, d_events, n, timestamp, auto_pulse=True):
         """After both gathers were summed: the batch (and its pulse when due, unless the caller

@@ -5,8 +5,9 @@
 out=gpurun_out/r4
 mkdir -p $out
 export TMPDIR=/tmp
-run() {  # name, limit, args...
+run() {  # name, limit, args... (ONLY: the names to run, default all)
   local name=$1 lim=$2; shift 2
+  if [ -n "$ONLY" ] && ! [[ " $ONLY " == *" $name "* ]]; then return 0; fi
   timeout -k 10 $lim python bench.py "$@" > $out/bench_$name.json 2> $out/bench_$name.err || { echo "FAIL $name rc=$?"; exit 1; }
   python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d.get('roofline') or {};print(sys.argv[2],d['value'],r.get('avg_launch_us'),r.get('frac'),(d.get('sync_commit') or {}).get('value'))" $out/bench_$name.json $name
 }
