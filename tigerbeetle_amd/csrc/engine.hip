@@ -1192,11 +1192,14 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   const uint32_t i0 = i - lane;  // the wave's first event
   uint4* ws = stage + (threadIdx.x >> 6) * 512;
   uint32_t cls = 0, code = TB_CT_OK;
-  bool ins = false;
+  bool ins = false, wdefer = false;
   if (i < E) {
     cls = s.cls[i];
     code = s.code[i];
-    ins = (cls & C_W) ? s.ins[i] != 0 : (cls & C_INSERTED) != 0;
+    const uint8_t wi = (cls & C_W) ? s.ins[i] : 0;
+    ins = (cls & C_W) ? wi != 0 : (cls & C_INSERTED) != 0;
+    // a component walker's commit: its balance effects are applied here (Walker::commit_record)
+    wdefer = XFER && wi == 2 && code == TB_CT_OK;
   }
   const uint32_t bad = code != TB_CT_OK;
   // The earlier segments' failure and insert counts, and this event's ranks inside the segment, in
@@ -1284,7 +1287,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
       // side, and a post's posted pair
       Add128 a_dr, a_cr, a_dr2, a_cr2;
       const bool small = d.g->small_win != 0;
-      if (!wev && (cls & C_COMMIT) && !(TBG_EXPERIMENTS && (o.xskip & 1))) {
+      if (((!wev && (cls & C_COMMIT)) || wdefer) && !(TBG_EXPERIMENTS && (o.xskip & 1))) {
         tb_account_t* dra = &d.acc[s.dr_slot[i]];
         tb_account_t* cra = &d.acc[s.cr_slot[i]];
         const u128 a = s.amt[i];
@@ -1302,7 +1305,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
             a_dr2.issue(&dra->debits_posted, a, small);
             a_cr2.issue(&cra->credits_posted, a, small);
           }
-          d.xstatus[s.p_tslot[i]] = (cls & C_POST) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
+          if (!wev) d.xstatus[s.p_tslot[i]] = (cls & C_POST) ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
         } else if (cls & C_PENDING) {
           a_dr.issue(&dra->debits_pending, a, small);
           a_cr.issue(&cra->credits_pending, a, small);

@@ -200,7 +200,8 @@ struct Walker {
     s.t2[i] = t2;
     s.hside[i] = 0;
     log_small(UNDO_INS, i, 0);
-    s.ins[i] = 1;
+    // 2: component mode, the balance effects are k_final's (an event committed iff ins and code ok)
+    s.ins[i] = atomic_bal ? 2 : 1;
     const uint32_t e = s.id_ent[i];
     // (the entry had no commit this window, or the caller would have found it: undo restores
     // "none", epoch 0, without reading the old word)
@@ -285,10 +286,8 @@ struct Walker {
     t.amount = W(amount);
     commit_record(i, t);
     if (atomic_bal) {
-      const bool pend = t.flags & TB_TRANSFER_PENDING;
-      add_bal(drs, pend ? 0 : 1, amount);
-      add_bal(crs, pend ? 2 : 3, amount);
-      if (pend) s.bstatus[i] = TB_PENDING_PENDING;
+      // the balance adds are k_final's (s.amt, the account slots: k_ct_prep's)
+      if (t.flags & TB_TRANSFER_PENDING) s.bstatus[i] = TB_PENDING_PENDING;
       return TB_CT_OK;
     }
     log_bal(drs);
@@ -369,12 +368,14 @@ struct Walker {
     }
     const u128 pa = U(p.amount);
     if (atomic_bal) {
-      add_bal(drs, 0, (u128)0 - pa);
-      add_bal(crs, 2, (u128)0 - pa);
-      if (t.flags & TB_TRANSFER_POST_PENDING) {
-        add_bal(drs, 1, amount);
-        add_bal(crs, 3, amount);
+      // the balance adds are k_final's: the amounts and, for a pending transfer of this window, its
+      // accounts (k_ct_prep wrote them for a stored one)
+      if (pc >= 0) {
+        s.dr_slot[i] = drs;
+        s.cr_slot[i] = crs;
       }
+      s.pamt[i] = pa;
+      s.amt[i] = amount;
       return TB_CT_OK;
     }
     tb_account_t* dra = &d.acc[drs];
