@@ -15,7 +15,7 @@
 // kept), then one walker thread per component (walker.h in atomic-balance mode, with a private undo
 // region). The window's sequential walker is skipped; k_walk only folds the outcomes.
 #pragma once
-#include "pwalker.h"
+#include "walker.h"
 
 __device__ inline bool cpw_active(const Globals* g) {
   // windows with history rows need the exact balances after each event: sequential walker
@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
     atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)st_n);
     atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)st_sum);
   }
-  if (!on || (XFER && len >= CW_LONG)) return;  // (long components: k_cc_walk_long)
+  if (!on) return;
   uint2* mine = pcache + threadIdx.x * WCACHE;
   for (int k = 0; k < WCACHE; k++) mine[k] = make_uint2(NONE32, 0);
   Walker wk;
@@ -155,24 +155,3 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
   wk.template run<XFER>(s.rval + start, len);
 }
 
-// Components of CW_LONG events or more (pwalker.h): one pipelined walker thread each, on the walk
-// stream beside k_cc_walk (64-thread blocks: the few long components spread over the CUs).
-__global__ void __launch_bounds__(64) k_cc_walk_long(Dev d, Scratch s, const uint8_t* ev, WinDesc w, uint32_t epoch) {
-  Globals* g = d.g;
-  if (!cpw_active(g)) return;
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= __hip_atomic_load(&g->cc_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  const uint32_t start = s.cc_list[j];
-  const uint32_t len = s.light[s.rkey[start]] + 1 - start;
-  if (len < CW_LONG) return;
-  PWalker wk;
-  wk.d = d;
-  wk.s = s;
-  wk.s.undo = s.undo + 5ull * start;
-  wk.ev = ev;
-  wk.w = &w;
-  wk.epoch = epoch;
-  wk.atomic_bal = true;
-  wk.small_bal = g->small_win != 0;  // k_prep_reduce
-  wk.run_x(s.rval + start, len);
-}
