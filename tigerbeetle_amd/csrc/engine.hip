@@ -1193,10 +1193,11 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   uint4* ws = stage + (threadIdx.x >> 6) * 512;
   uint32_t cls = 0, code = TB_CT_OK;
   bool ins = false, wdefer = false;
+  uint8_t wi = 0;  // W events: 1 sequential walker, 2 component walker (Walker::commit_record)
   if (i < E) {
     cls = s.cls[i];
     code = s.code[i];
-    const uint8_t wi = (cls & C_W) ? s.ins[i] : 0;
+    wi = (cls & C_W) ? s.ins[i] : 0;
     ins = (cls & C_W) ? wi != 0 : (cls & C_INSERTED) != 0;
     // a component walker's commit: its balance effects are applied here (Walker::commit_record)
     wdefer = XFER && wi == 2 && code == TB_CT_OK;
@@ -1256,7 +1257,9 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
   // its live expires_at entry, if any (appended per wave below: one counter atomic per wave)
   bool xapp = false;
   ExpEntry xent;
-  if (XFER && (cls & C_W)) {
+  // a component walker's create: its input row, stamped (the walker stored no record)
+  const bool wcreate = XFER && wi == 2 && !(cls & C_POSTVOID);
+  if (XFER && (cls & C_W) && !wcreate) {
     const uint4* t2 = reinterpret_cast<const uint4*>(&s.t2[i]);
 #pragma unroll
     for (int q = 0; q < 8; q++) rec[q] = t2[q];
@@ -1324,11 +1327,9 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
         d.xstatus[slot] = 0;
       } else if (ins) {
         const uint64_t slot = xbase + rins;
-        if (!wev) {
-          rw_stamp(rec, win_ts(w, b, i));
-          if (cls & C_POSTVOID) rw_post_void(rec, &d.xr[s.p_tslot[i]], s.amt[i]);
-        }
-        if (wev && s.hside[i]) {  // historical_balance row (the walker computed it)
+        if (!wev || wcreate) rw_stamp(rec, win_ts(w, b, i));
+        if (!wev && (cls & C_POSTVOID)) rw_post_void(rec, &d.xr[s.p_tslot[i]], s.amt[i]);
+        if (wev && wi == 1 && s.hside[i]) {  // historical_balance row (the walker computed it)
           d.hist[slot] = s.hrow[i];
           d.hist_side[slot] = s.hside[i];
         }

@@ -196,18 +196,26 @@ struct Walker {
     s.hside[i] = side;
   }
 
-  __device__ __attribute__((always_inline)) void commit_record(uint32_t i, const tb_transfer_t& t2) {
-    s.t2[i] = t2;
-    s.hside[i] = 0;
+  // Event i's record t2 (pv: a posting record) and its id's commit (key-map entry e). A component
+  // walker (atomic_bal) stores no record for a create: k_final stamps the input row, and a later
+  // reader here takes the input row too (walk_record); nor a history side (none in its windows).
+  __device__ __attribute__((always_inline)) void commit_record(uint32_t i, uint32_t e, const tb_transfer_t& t2, bool pv) {
+    if (!atomic_bal || pv) s.t2[i] = t2;
+    if (!atomic_bal) s.hside[i] = 0;
     log_small(UNDO_INS, i, 0);
     // 2: component mode, the balance effects are k_final's (an event committed iff ins and code ok)
     s.ins[i] = atomic_bal ? 2 : 1;
-    const uint32_t e = s.id_ent[i];
     // (the entry had no commit this window, or the caller would have found it: undo restores
     // "none", epoch 0, without reading the old word)
     log_small(UNDO_COMMIT, e, 0);
     bmap_set_committed(s.bmap, e, epoch, (int32_t)i);
     if (pcache) pcache[e & (WCACHE - 1)] = make_uint2(e, i);
+  }
+
+  // The record event c committed earlier in the window (the exists checks compare no timestamp).
+  __device__ __attribute__((always_inline)) const tb_transfer_t& walk_record(int32_t c) const {
+    if (atomic_bal && !(s.cls[c] & C_POSTVOID)) return reinterpret_cast<const tb_transfer_t*>(ev)[c];
+    return s.t2[c];
   }
 
   template <bool XFER>
@@ -264,7 +272,7 @@ struct Walker {
     t.timestamp = win_ts(*w, e.b, i);
     if (pv) return post_or_void(e, t, c, pc);
     if (e.id_tslot != NONE32) return ct_exists(t, d.xr[e.id_tslot]);
-    if (c >= 0) return ct_exists(t, s.t2[c]);
+    if (c >= 0) return ct_exists(t, walk_record(c));
     const uint32_t drs = e.dr, crs = e.cr;
     tb_account_t* dra = &d.acc[drs];
     tb_account_t* cra = &d.acc[crs];
@@ -284,7 +292,7 @@ struct Walker {
       if (r != TB_CT_OK) return r;
     }
     t.amount = W(amount);
-    commit_record(i, t);
+    commit_record(i, e.id_ent, t, false);
     if (atomic_bal) {
       // the balance adds are k_final's (s.amt, the account slots: k_ct_prep's)
       if (t.flags & TB_TRANSFER_PENDING) s.bstatus[i] = TB_PENDING_PENDING;
@@ -314,7 +322,7 @@ struct Walker {
                                                                   int32_t pc) {
     const uint32_t i = e.i;
     const uint32_t pslot = e.p_tslot;
-    uint32_t drs, crs;
+    uint32_t drs, crs, pb = NONE32;  // pb: the in-window pending transfer's batch (from its row)
     uint8_t pst0;
     const tb_transfer_t* pp;  // one load from the selected record (no merged aggregate)
     if (pslot != NONE32) {
@@ -324,28 +332,31 @@ struct Walker {
       pst0 = d.xstatus[pslot];
     } else {
       if (pc < 0) return TB_CT_PENDING_TRANSFER_NOT_FOUND;
-      pp = &s.t2[pc];
+      // (a component walker stored no record for it: its input row, stamped below)
+      pp = atomic_bal ? reinterpret_cast<const tb_transfer_t*>(ev) + pc : &s.t2[pc];
       if (rows) {
         const uint4 r1 = s.wrow[2 * pc + 1];
         drs = r1.x;
         crs = r1.y;
+        pb = r1.w;
       } else {
         drs = s.dr_slot[pc];
         crs = s.cr_slot[pc];
       }
       pst0 = s.bstatus[pc];
     }
-    const tb_transfer_t p = *pp;
+    tb_transfer_t p = *pp;
+    if (atomic_bal && pslot == NONE32) p.timestamp = win_ts(*w, pb == NONE32 ? s.batch[pc] : pb, (uint32_t)pc);
     u128 amount;
     uint32_t r = pv_against(t, p, &amount);
     if (r != CONT) return r;
     if (e.id_tslot != NONE32) return pv_exists(t, d.xr[e.id_tslot], p);
-    if (c >= 0) return pv_exists(t, s.t2[c], p);
+    if (c >= 0) return pv_exists(t, walk_record(c), p);
     uint8_t pst = pst0;
     if (pst == TB_PENDING_PENDING && xw_expired_before(*w, p, s.batch[i])) pst = TB_PENDING_EXPIRED;
     r = pv_status(pst);
     if (r != CONT) return r;
-    commit_record(i, pv_record(t, p, amount));
+    commit_record(i, e.id_ent, pv_record(t, p, amount), true);
     if (p.timeout > 0 && expires_at_of(p) <= t.timestamp) return TB_CT_PENDING_TRANSFER_EXPIRED;
     if (pc >= 0 && p.timeout > 0) {
       // p was created in this window (k_ct_prep could not see it): the expires_at removal and the
