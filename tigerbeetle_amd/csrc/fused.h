@@ -116,6 +116,11 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
           const uint64_t hx = hash_id(t.id.lo, t.id.hi);
           const AccEntry ed = d.acc_tab[hd], ec = d.acc_tab[hc];
           const XEntry ex = mx ? d.x_tab[hx & d.x_mask] : X_EMPTY;
+          // claim mode: the claim goes out behind the probes' first loads (one counter orders a
+          // wave's loads and atomics: issued earlier, the returning atomic would hold up their use).
+          // An event that then fails the account checks has claimed its id too: a later duplicate of
+          // it sends the window to the general path, which decides it exactly.
+          const bool dup = claim && fu_claim(bm, bmask, evb, t.id, i, tag);
           AccEntry de, ce;
           o->dr = acc_probe_from(d.acc_tab, d.acc_mask, hd, ed, t.debit_account_id, &de);
           o->cr = acc_probe_from(d.acc_tab, d.acc_mask, hc, ec, t.credit_account_id, &ce);
@@ -133,7 +138,7 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
             if (((de.flags | ce.flags) & TB_ACCOUNT_HISTORY) || (de.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) ||
                 (ce.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) || t.amount.hi != 0 || t.amount.lo >= FU_AMOUNT_MAX)
               simple = false;
-            if (claim && fu_claim(bm, bmask, evb, t.id, i, tag)) simple = false;  // in-window duplicate
+            if (dup) simple = false;  // in-window duplicate
             uint32_t xs = mx ? x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id) : NONE32;
             if (xs == NONE32 && mx) xs = x_prefix_find(d.xr, P, t.id);
             // :1506-1507; a plain create with timeout 0 cannot overflow the timeout (:1543)
