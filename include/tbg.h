@@ -294,7 +294,8 @@ int tbg_shard_gather(tbg_engine *engine, uint32_t operation, const void *d_event
  * batch by batch), plus each shard's smallest live entry beyond t_last; phase 2 the accounts of the
  * gathered pending and due transfers. Asynchronous, no host round trip. After both sums,
  * tbg_gathered_objects writes the distinct gathered objects in timestamp order (sorted and
- * deduplicated on the device; synchronous: the counts size the scratch engine's tbg_open_device),
+ * deduplicated on the device on the timestamp bits below t_last's, so on the engine that ran this
+ * window's phase 1; synchronous: the counts size the scratch engine's tbg_open_device),
  * the scratch engine commits the whole window (tbg_commit_window: the pulses inside it modelled as on
  * one engine, or TBG_E_WINDOW at tbg_sync, then nothing is applied and the window goes batch by
  * batch), and tbg_shard_apply keeps the owned objects. Replaces tbg_shard_gather per batch; the

@@ -229,7 +229,8 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
                                                  uint32_t epoch) {
   __shared__ u128 red[256];
   __shared__ uint4 stage[256 * 4];  // half of each event's record (16 KiB): the in-place record store
-  // bit 0 huge amount, bit 1 not claim-free, bit 2 first id above every stored id, bit 3 pulse_next op
+  // bit 0 huge amount, bit 1 ids not strictly increasing, bit 6 a post/void (either: not claim-free),
+  // bit 2 first id above every stored id, bit 3 pulse_next op
   __shared__ uint32_t aux;
   __shared__ u128 id_max[256 / 64];  // per wave: largest id this block may insert (Globals::x_id_max)
   __shared__ uint32_t marked[MARK_LDS];  // mark_first: accounts this block marks
@@ -256,10 +257,10 @@ __global__ void __launch_bounds__(256) k_ct_prep(Dev d, Scratch s, const tb_tran
     const uint8_t* evb = reinterpret_cast<const uint8_t*>(ev);
     const uint32_t b = win_batch(w, i);
     {
-      // claim-free: ids strictly increasing (u128 order) over the window, no post/void
-      bool nf = (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
-      if (i > 0) nf |= !(U(t.id) > U(ev[i - 1].id));
-      if (nf) atomicOr(&aux, 2u);
+      // claim-free: ids strictly increasing (u128 order) over the window (bit 1) and no post/void
+      // (bit 6); the records extend the sorted prefix with rising fresh ids, post/voids or not
+      if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) atomicOr(&aux, 64u);
+      if (i > 0 && !(U(t.id) > U(ev[i - 1].id))) atomicOr(&aux, 2u);
       if (i == 0 && U(t.id) > x_id_max) atomicOr(&aux, 4u);
     }
     uint32_t cls = 0, code;
@@ -527,8 +528,8 @@ __global__ void __launch_bounds__(1024) k_prep_reduce(Dev d, Scratch s, uint32_t
     Globals* g = d.g;
     g->batch_amount_sum += tot;
     if (aux & 1u) g->batch_huge = 1;
-    const bool claim_free = !(aux & 2u);
-    const bool prefix = claim_free && (aux & 4u) && g->x_sorted == g->x_count;
+    const bool claim_free = !(aux & (2u | 64u));
+    const bool prefix = !(aux & 2u) && (aux & 4u) && g->x_sorted == g->x_count;
     // bit 2: pulse_next ops; bit 3: a post/void that may reset pulse_next (k_final replays the
     // window's ops in order only then; else pulse_next = min(itself, the creations that ran ok))
     // bit 4: history rows: the sequential walker (exact balances after each event) decides W
