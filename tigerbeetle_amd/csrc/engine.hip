@@ -56,11 +56,6 @@ using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::def
 #ifndef TBG_NT_LOAD
 #define TBG_NT_LOAD 1
 #endif
-// TBG_EXPERIMENTS=1 builds a timing-experiment library (TBG_EXPERIMENT_SKIP switches parts of
-// k_final off; results are then wrong). Release builds compile the switches out.
-#ifndef TBG_EXPERIMENTS
-#define TBG_EXPERIMENTS 0
-#endif
 #ifndef TBG_NT_STORE
 #define TBG_NT_STORE 1
 #endif
@@ -1103,8 +1098,6 @@ struct FinalOut {
   tb_create_result_t* results;  // window replies, concatenated per batch
   uint32_t* batch_base;         // [nb + 1]: batch b's replies are results[base[b] .. base[b+1])
   uint32_t* out_count;          // optional: total failures (single-batch callers)
-  uint32_t xskip;               // timing experiments only (TBG_EXPERIMENT_SKIP; results are wrong):
-                                // 1 balance atomics, 2 id-table insert, 4 record store
 };
 
 // A 128-bit atomic add split in two phases so that several can be in flight before any carry is
@@ -1291,7 +1284,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
       // side, and a post's posted pair
       Add128 a_dr, a_cr, a_dr2, a_cr2;
       const bool small = d.g->small_win != 0;
-      if (((!wev && (cls & C_COMMIT)) || wdefer) && !(TBG_EXPERIMENTS && (o.xskip & 1))) {
+      if ((!wev && (cls & C_COMMIT)) || wdefer) {
         tb_account_t* dra = &d.acc[s.dr_slot[i]];
         tb_account_t* cra = &d.acc[s.cr_slot[i]];
         const u128 a = s.amt[i];
@@ -1335,7 +1328,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
           d.hist_side[slot] = s.hside[i];
         }
         // records of a prefix-extending window are found by binary search (x_prefix_find)
-        if (!(TBG_EXPERIMENTS && (o.xskip & 2)) && !prefix_win) x_insert(d.x_tab, d.x_mask, rw_u128(rec[0]), (uint32_t)slot);
+        if (!prefix_win) x_insert(d.x_tab, d.x_mask, rw_u128(rec[0]), (uint32_t)slot);
         uint8_t st = 0;
         if ((rec[7].y >> 16) & TB_TRANSFER_PENDING) {
           st = wev ? s.bstatus[i] : (uint8_t)TB_PENDING_PENDING;
@@ -1391,10 +1384,9 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     for (int q = 0; q < 8; q++) ws[(rins - r0) * 8 + q] = rec[q];
   }
   wave_sync();
-  if (!(TBG_EXPERIMENTS && (o.xskip & 4))) {
-    uint4* dst = reinterpret_cast<uint4*>(XFER ? (void*)d.xr : (void*)d.acc) + (size_t)(xbase + r0) * 8;
-    for (uint32_t k = lane; k < nins * 8; k += 64) st_stream(dst + k, ws[k]);
-  }
+  uint4* dst = reinterpret_cast<uint4*>(XFER ? (void*)d.xr : (void*)d.acc) + (size_t)(xbase + r0) * 8;
+  for (uint32_t k = lane; k < nins * 8; k += 64) st_stream(dst + k, ws[k]);
+
   if (i == E - 1) {
     // the window's last event: totals and window-level state
     const uint32_t total_bad = rbad + bad, total_ins = rins + (ins ? 1u : 0u);

@@ -161,14 +161,13 @@ struct FuScratch {
   unsigned long long* ok;   // per wave: ok-event bitmap
 };
 
-__device__ __forceinline__ void fu_store_records(Dev d, const tb_transfer_t& t, bool ok, unsigned long long okm,
+__device__ __forceinline__ void fu_store_records(Dev d, const uint4* src, bool ok, unsigned long long okm,
                                                  uint64_t first_slot, uint4* ws) {
   // the wave's ok records as one contiguous run from first_slot, through LDS in two halves of 64 B
   // (each store instruction writes whole 64 B sectors)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nins = (uint32_t)__popcll(okm);
   const uint32_t pos = ok ? (uint32_t)__popcll(okm & ((1ull << lane) - 1ull)) : 0u;
-  const uint4* src = reinterpret_cast<const uint4*>(&t);
   uint4* dst = reinterpret_cast<uint4*>(d.xr + first_slot);
 #pragma unroll
   for (int half = 0; half < 2; half++) {
@@ -302,7 +301,7 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   if (ok) d.xstatus[base + i] = 0;
   if (okm) {  // in place: slot base + i
     const uint32_t first = (uint32_t)__builtin_ctzll(okm);
-    fu_store_records(d, t, ok, okm, base + (i - lane) + first, stage + wave * 256);
+    fu_store_records(d, reinterpret_cast<const uint4*>(&t), ok, okm, base + (i - lane) + first, stage + wave * 256);
   }
   // this block's failures, reaching amounts' sum and largest reaching id (k_fu_final folds them)
   const uint32_t wbad = (uint32_t)__popcll(__ballot(bad));
@@ -424,15 +423,18 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
   if (__ballot(ok && rbad != 0)) {
     // an earlier event failed: this wave's records move down to their ranks (from the input; the
     // branch is wave-uniform, so the run's store loop has every lane)
-    tb_transfer_t t;
+    // (the record as 16 B words, not a struct whose address is taken: that put it in scratch memory)
+    uint4 rec[8];
+    const uint4* src = reinterpret_cast<const uint4*>(ev) + (size_t)i * 8;
+#pragma unroll
+    for (int q = 0; q < 8; q++) rec[q] = ok ? src[q] : make_uint4(0, 0, 0, 0);
     if (ok) {
-      t = ev[i];
-      t.timestamp = win_ts(w, win_batch(w, i), i);
+      rw_stamp(rec, win_ts(w, win_batch(w, i), i));
       d.xstatus[base + rins] = 0;
     }
     const unsigned long long okm = __ballot(ok);
     const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, (int)__builtin_ctzll(okm));
-    fu_store_records(d, t, ok, okm, base + r0, stage + wave * 256);
+    fu_store_records(d, rec, ok, okm, base + r0, stage + wave * 256);
   }
   if (ok && !prefix_win) x_insert(d.x_tab, d.x_mask, ev[i].id, (uint32_t)(base + rins));
   if (k == gridDim.x - 1) {
