@@ -38,7 +38,8 @@
                         // (others share the SIMD); 0: taken from the long queue like any other
 #endif
 #ifndef RC_PROF
-#define RC_PROF 0  // 1: per-phase clock64() sums of k_rc_run into Globals::dbg (tbg_debug_counters)
+#define RC_PROF 0  // 1: per-phase clock64() sums of k_rc_run into Globals::dbg (tbg_debug_counters);
+                   // profiling only: it adds clock reads and changes no result
 #endif
 #define RC_NONE 0xFFFFu
 
