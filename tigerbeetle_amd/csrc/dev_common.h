@@ -146,7 +146,7 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t fu_windows;  // cumulative windows committed by the fused pass
   uint32_t fu_fail_epoch;  // the fused-only window that left the class (window_error bit 3)
   uint32_t sh_mis;         // sharded: this shard's ledger-mismatch slots used this window (shard.h)
-  uint32_t sh_unsup;       // sharded: a home event outside the class this window (k_sh_count -> trailer 2)
+  uint32_t sh_unsup;       // sharded: a home event outside the class this window (k_sh_reply -> trailer 2)
   uint64_t ovf_rescans;    // times ovf_bound was re-tightened to the accounts' largest balance sum (restore.h)
   uint32_t fu_nonmono;     // the epoch of a fused window whose ids did not all rise (claim mode, fused.h)
   uint32_t pad5;

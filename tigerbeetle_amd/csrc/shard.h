@@ -21,7 +21,8 @@
 //   k_sh_home_*   home slice: validation codes and class checks.
 //   k_sh_decide   home slice: account lookups (:1496-1497), ledgers (:1503-1504), exists, then linked
 //                 chains (:1240-1300).
-//   k_sh_count, k_sh_reply   home slice: per-batch replies; one commit bit per event (exchange 2).
+//   k_sh_reply    home slice: per-batch replies (failure ranks from k_sh_decide's per-segment
+//                 counts); one commit bit per event (exchange 2).
 //   (caller)      exchange 2: byte-wise sum all-reduce of the commit bits (E/8 B) and home verdicts.
 //   k_sh_icount, k_sh_apply  whole window, owned roles only: the verdict, then the account owners add
 //                 the amounts (exact 128-bit atomics) and the id owner appends the record.
@@ -273,7 +274,7 @@ __global__ void __launch_bounds__(SEG) k_sh_roles(Dev d, Scratch s, const uint8_
   const uint32_t i = blockIdx.x * SEG + threadIdx.x;
   if (threadIdx.x == 0) aux = 0;
   // exchange 1's trailer (written by later kernels of the window only): zeroed here, not by a memset;
-  // so is the homes' out-of-class flag that k_sh_count turns into exchange 2's trailer
+  // so is the homes' out-of-class flag that k_sh_reply turns into exchange 2's trailer
   if (i < 4) xch.trailer[i] = 0;
   if (i == 0) d.g->sh_unsup = 0;
   __syncthreads();
@@ -469,6 +470,9 @@ __global__ void __launch_bounds__(256) k_sh_home(Scratch s, const uint8_t* __res
   // every commit-bit word of the window starts at zero (k_sh_reply writes this home's words; the
   // all-reduce sums every shard's): zeroed here rather than by a memset launch
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nwords; k += gridDim.x * blockDim.x) bits[k] = 0;
+  // so do the home segments' failure counts (k_sh_decide adds to them)
+  const uint32_t nseg = (e1 - 1) / SEG - e0 / SEG + 1;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nseg; k += gridDim.x * blockDim.x) s.cnt_bad[k] = 0;
   const uint32_t i = e0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= e1) return;
   const uint32_t b = win_batch(w, i);
@@ -524,10 +528,12 @@ __global__ void __launch_bounds__(256) k_sh_decide(Scratch s, const uint8_t* ev,
   const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
   if (i != first && (s.cls[i - 1] & C_LINKED)) return;  // chain member: its head decides
   const uint32_t cls = s.cls[i];
+  const uint32_t k0 = e0 / SEG;  // failures per home segment (s.cnt_bad[seg - k0]: k_sh_reply's ranks)
   if (!(cls & C_LINKED)) {
     const uint32_t code = sh_code<XFER>(s, ev, xch, i, trailer2);
     s.code[i] = code;
     if (code == TB_CT_OK) s.cls[i] = cls | C_COMMIT;
+    else atomicAdd(&s.cnt_bad[i / SEG - k0], 1u);
     return;
   }
   // chain head: members i..end (:1240-1300). No member's outcome depends on another member's
@@ -550,26 +556,21 @@ __global__ void __launch_bounds__(256) k_sh_decide(Scratch s, const uint8_t* ev,
       s.code[j] = TB_CT_LINKED_EVENT_FAILED;  // back-fill before f, broken chain after f
     }
   }
-}
-
-// Home slice, per segment k0 + blockIdx.x (segments are window-aligned, SEG events): failure counts.
-__global__ void __launch_bounds__(SEG) k_sh_count(Scratch s, uint32_t e0, uint32_t e1, uint32_t k0,
-                                                  const uint32_t* unsup, uint32_t* trailer2) {
-  __shared__ uint32_t lds[SEG / 64];
-  // exchange 2's trailer from the homes' flag (k_sh_home / k_sh_decide, earlier launches): written
-  // whole here instead of a memset before them
-  if (blockIdx.x == 0 && threadIdx.x < 4) trailer2[threadIdx.x] = threadIdx.x == 0 ? *unsup : 0u;
-  const uint32_t i = (k0 + blockIdx.x) * SEG + threadIdx.x;
-  const uint32_t nbad = (i >= e0 && i < e1 && s.code[i] != TB_CT_OK) ? 1u : 0u;
-  const uint32_t tot = block_sum<SEG / 64>(nbad, lds);
-  if (threadIdx.x == 0) s.cnt_bad[blockIdx.x] = tot;
+  if (f != NONE32) {  // every member failed; the chain may span several segments
+    for (uint32_t g = i / SEG; g <= end / SEG; g++)
+      atomicAdd(&s.cnt_bad[g - k0], std::min(end + 1, (g + 1) * SEG) - std::max(i, g * SEG));
+  }
 }
 
 // Home slice: replies of batches [hb0, hb1) (batch_base relative to hb0, indices batch-relative) and
 // the commit bit of every slice event (one 64-bit word per wave; words are window-aligned).
 __global__ void __launch_bounds__(SEG) k_sh_reply(Dev d, Scratch s, WinDesc w, uint32_t hb0, uint32_t hb1, uint32_t e0,
-                                                  uint32_t e1, uint32_t k0, FinalOut o, unsigned long long* bits) {
+                                                  uint32_t e1, uint32_t k0, FinalOut o, unsigned long long* bits,
+                                                  const uint32_t* unsup, uint32_t* trailer2) {
   __shared__ uint32_t lds[SEG / 64];
+  // exchange 2's trailer from the homes' flag (k_sh_home / k_sh_decide, earlier launches): written
+  // whole here instead of a memset before them
+  if (blockIdx.x == 0 && threadIdx.x < 4) trailer2[threadIdx.x] = threadIdx.x == 0 ? *unsup : 0u;
   const uint32_t i = (k0 + blockIdx.x) * SEG + threadIdx.x;
   const bool mine = i >= e0 && i < e1;
   uint32_t cls = 0, code = TB_CT_OK;
