@@ -168,10 +168,12 @@ void *tbg_stream(tbg_engine *engine);
  *   3. tbg_shard_decide_window: decides the home batches [home_first, home_first + home_count) from
  *      the summed facts; writes their replies (d_results / d_batch_base as tbg_commit_window, for the
  *      home batches only, d_batch_base[0..home_count]) and one commit bit per window event at
- *      d_commit_bits (tbg_shard_commit_bits_bytes(E) bytes: 16 B trailer + E bits, zero outside the
- *      home batches);
+ *      d_commit_bits (tbg_shard_commit_bits_bytes(E) bytes: a 16 B trailer of this shard's verdicts
+ *      as a home and as an owner, whose sum over the shards is nonzero when the window leaves the
+ *      class, then E bits, zero outside the home batches);
  *   4. the caller sums the commit-bit bytes across the shards in place, as in 2;
- *   5. tbg_shard_commit_window: applies only the owned effects of the committed events.
+ *   5. tbg_shard_commit_window: applies only the owned effects of the committed events (the verdict
+ *      is the summed trailer of step 4; d_exchange is no longer read, kept for the ABI).
  * Sharded class: create_accounts and create_transfers without limits, balancing, two-phase or
  * in-window duplicate ids, overflow-free. Any other window is rejected whole on every shard:
  * tbg_sync returns TBG_E_UNSUPPORTED and no shard has applied it. Asynchronous on the engine stream. */

@@ -15,15 +15,16 @@
 //                 with a stored transfer (`exists`, :1506-1507). The debit / credit owners read the
 //                 account ids and the amount and resolve their account (ledger, limit flag). Each
 //                 owner writes its part of the event's 9 B of facts (exchange 1).
-//   k_sh_close    one block: folds the scan blocks' partials (capacity, overflow bound, prefix flag).
 //   (caller)      exchange 1: byte-wise sum all-reduce of the facts (RCCL over xGMI). Every bit has
 //                 exactly one writer, so the sum is the union.
 //   k_sh_home_*   home slice: validation codes and class checks.
 //   k_sh_decide   home slice: account lookups (:1496-1497), ledgers (:1503-1504), exists, then linked
 //                 chains (:1240-1300).
 //   k_sh_reply    home slice: per-batch replies (failure ranks from k_sh_decide's per-segment
-//                 counts); one commit bit per event (exchange 2).
-//   (caller)      exchange 2: byte-wise sum all-reduce of the commit bits (E/8 B) and home verdicts.
+//                 counts); one commit bit per event (exchange 2). Block 0 folds the owned work's
+//                 partials into this shard's owner verdicts (k_sh_close does it for a shard home to
+//                 no event).
+//   (caller)      exchange 2: byte-wise sum all-reduce of the commit bits (E/8 B) and the verdicts.
 //   k_sh_icount, k_sh_apply  whole window, owned roles only: the verdict, then the account owners add
 //                 the amounts (exact 128-bit atomics) and the id owner appends the record.
 //
@@ -31,8 +32,8 @@
 // account, no balancing), no history row (no flags.history on a touched account), no two-phase, no
 // in-window duplicate id, overflow-free window. Then every
 // event's outcome is a function of the owners' facts alone, and the effects commute. A window outside
-// the class is detected before anything is applied (by an owner: exchange 1's trailer; by a home:
-// exchange 2's trailer), so every shard reaches the same verdict and the window fails with
+// the class is detected before anything is applied (by an owner or a home: exchange 2's trailer), so
+// every shard reaches the same verdict and the window fails with
 // TBG_E_UNSUPPORTED at tbg_sync: no shard applies any of it.
 #pragma once
 #include "changes.h"
@@ -42,9 +43,7 @@
 
 // Exchange bytes of a window of E events over G shards (summed byte-wise over the shards: every bit
 // has exactly one writer, so the byte sum is the union with no carries; one uint8 all-reduce):
-//   [0, 16)         trailer, 4 x u32: shards that saw an unsupported event (or overflowed their
-//                   ledger-mismatch slots), shards over capacity, shards whose overflow bound does not
-//                   clear the window's amounts, unused
+//   [0, 16)         trailer: unused, zero (the owners' verdicts travel in exchange 2's)
 //   [16, 16+E)      bits 0-5: 1 + (TB_CT_OK or the exists* code; create_accounts: 1 + the code), by
 //                   the id owner; bit 6: the debit account has debits_must_not_exceed_credits or
 //                   flags.history (its owner); bit 7: the credit account has
@@ -159,8 +158,10 @@ __device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bo
   g->batch_huge = 0;
 }
 
-// Exchange 2 (commit bits): 16 B trailer (u32 [0]: homes that found an event outside the class),
-// then one bit per event, in 64-bit words (a word may hold bits of two homes: distinct bits).
+// Exchange 2 (commit bits): 16 B trailer, 4 x u32 summed over the shards: [0] homes that found an
+// event outside the class, [1] shards that saw an in-window duplicate id or overflowed their
+// ledger-mismatch slots, [2] shards over capacity, [3] shards whose overflow bound does not clear
+// the window's amounts; then one bit per event, in 64-bit words (a word may hold bits of two homes: distinct bits).
 __host__ __device__ inline uint64_t xch2_bytes(uint32_t E) { return 16 + 8ull * ((E + 63) / 64); }
 
 // Scan-block partials (Scratch::blk_aux): bit 0 huge amount, bit 1 in-window duplicate id (outside the
@@ -168,17 +169,17 @@ __host__ __device__ inline uint64_t xch2_bytes(uint32_t E) { return 16 + 8ull * 
 // stored id, owned ids reaching the exists check << 4.
 enum : uint32_t { SHX_HUGE = 1, SHX_DUP = 2, SHX_NONMONO = 4, SHX_FRESH = 8, SHX_OWN_SHIFT = 4 };
 
-// After the scan (stream-ordered, one block): folds the scan blocks' partials (no same-address
-// atomics across blocks) into the window's local verdicts: trailer words 0 (duplicate id), 1
-// (capacity), 2 (overflow bound); Globals::win_flags bit 1 (the owned records extend the sorted
-// prefix). (A separate launch, not a last-block pattern: no device fences in the sharded kernels.)
-__global__ void __launch_bounds__(1024) k_sh_close(Dev d, Scratch s, uint32_t nblk, uint32_t* trailer, uint32_t xfer) {
-  __shared__ u128 red[1024];
-  __shared__ uint32_t bits;
-  __shared__ unsigned long long own_s;
+// After exchange 1 (stream-ordered, one 1024-thread block: block 0 of k_sh_reply, or k_sh_close when
+// this shard is home to no event): folds the scan blocks' partials (no same-address atomics across
+// blocks) into this shard's window verdicts, returned to thread 0 as bit 0 (duplicate id or
+// mismatch slots overflowed), bit 1 (capacity), bit 2 (overflow bound), and sets
+// Globals::win_flags bit 1 (the owned records extend the sorted prefix) and small_win for k_sh_apply.
+// The verdicts travel in exchange 2's trailer, so exchange 1 needs no fold before it.
+__device__ inline uint32_t sh_close_fold(Dev d, const Scratch& s, uint32_t nblk, uint32_t xfer, u128* red,
+                                         uint32_t* bits_s, unsigned long long* own_s) {
   if (threadIdx.x == 0) {
-    bits = 0;
-    own_s = 0;
+    *bits_s = 0;
+    *own_s = 0;
   }
   __syncthreads();
   u128 v = 0;
@@ -190,25 +191,46 @@ __global__ void __launch_bounds__(1024) k_sh_close(Dev d, Scratch s, uint32_t nb
     own += x >> SHX_OWN_SHIFT;
     if (xfer) v += s.blk_amt[j];
   }
-  if (a) atomicOr(&bits, a);
-  if (own) atomicAdd(&own_s, own);
+  if (a) atomicOr(bits_s, a);
+  if (own) atomicAdd(own_s, own);
+  __syncthreads();  // (the LDS atomics above, before thread 0 reads them)
   const u128 tot = xfer ? block_sum_u128(v, red) : (u128)0;
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x != 0) return 0;
   Globals* g = d.g;
-  if (bits & SHX_DUP) trailer[0] = 1;
+  const uint32_t bits = *bits_s;
+  uint32_t verdict = (bits & SHX_DUP) ? 1u : 0u;
   if (xfer) {
     g->batch_amount_sum += tot;
     if (bits & SHX_HUGE) g->batch_huge = 1;
-    if (g->x_count + own_s > d.x_max) trailer[1] = 1;
-    if (window_ovf_mode(g)) trailer[2] = 1;
+    if (g->x_count + *own_s > d.x_max) verdict |= 2u;
+    if (window_ovf_mode(g)) verdict |= 4u;
     // every owned balance field stays below 2^64 this window: k_sh_apply's adds need no carry
     const u128 top = g->ovf_bound + g->batch_amount_sum;
     g->small_win = (!g->batch_huge && top >= g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1u : 0u;
     const bool prefix = !(bits & SHX_NONMONO) && (bits & SHX_FRESH) && g->x_sorted == g->x_count;
     g->win_flags = prefix ? 2u : 0u;
   } else {
-    if (g->acc_count + own_s > d.acc_max) trailer[1] = 1;
+    if (g->acc_count + *own_s > d.acc_max) verdict |= 2u;
   }
+  return verdict;
+}
+
+// Exchange 2's trailer, written whole by thread 0: the homes' out-of-class flag (k_sh_home /
+// k_sh_decide) and this shard's owner verdicts (sh_close_fold), one word each.
+__device__ inline void sh_trailer2(uint32_t* trailer2, uint32_t unsup, uint32_t verdict) {
+  trailer2[0] = unsup;
+  trailer2[1] = verdict & 1u;
+  trailer2[2] = (verdict >> 1) & 1u;
+  trailer2[3] = (verdict >> 2) & 1u;
+}
+
+// A shard home to no event of the window still folds its owner verdicts into exchange 2.
+__global__ void __launch_bounds__(1024) k_sh_close(Dev d, Scratch s, uint32_t nblk, uint32_t xfer, uint32_t* trailer2) {
+  __shared__ u128 red[1024];
+  __shared__ uint32_t bits_s;
+  __shared__ unsigned long long own_s;
+  const uint32_t verdict = sh_close_fold(d, s, nblk, xfer, red, &bits_s, &own_s);
+  if (threadIdx.x == 0) sh_trailer2(trailer2, 0u, verdict);
 }
 
 // Validation a create_transfers event gets on every shard that looks at it whole (its owners and its
@@ -421,7 +443,7 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
   }
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  if (threadIdx.x == 0) {  // this segment's partials (k_sh_close folds them)
+  if (threadIdx.x == 0) {  // this segment's partials (sh_close_fold folds them)
     u128 tot = 0;
 #pragma unroll
     for (int w2 = 0; w2 < SEG / 64; w2++) tot += red[w2];
@@ -566,11 +588,16 @@ __global__ void __launch_bounds__(256) k_sh_decide(Scratch s, const uint8_t* ev,
 // the commit bit of every slice event (one 64-bit word per wave; words are window-aligned).
 __global__ void __launch_bounds__(SEG) k_sh_reply(Dev d, Scratch s, WinDesc w, uint32_t hb0, uint32_t hb1, uint32_t e0,
                                                   uint32_t e1, uint32_t k0, FinalOut o, unsigned long long* bits,
-                                                  const uint32_t* unsup, uint32_t* trailer2) {
+                                                  const uint32_t* unsup, uint32_t* trailer2, uint32_t nscan,
+                                                  uint32_t xfer) {
   __shared__ uint32_t lds[SEG / 64];
-  // exchange 2's trailer from the homes' flag (k_sh_home / k_sh_decide, earlier launches): written
-  // whole here instead of a memset before them
-  if (blockIdx.x == 0 && threadIdx.x < 4) trailer2[threadIdx.x] = threadIdx.x == 0 ? *unsup : 0u;
+  __shared__ u128 red[SEG];
+  __shared__ uint32_t bits_s;
+  __shared__ unsigned long long own_s;
+  if (blockIdx.x == 0) {  // (block-uniform) exchange 2's trailer, instead of a memset before the homes
+    const uint32_t verdict = sh_close_fold(d, s, nscan, xfer, red, &bits_s, &own_s);
+    if (threadIdx.x == 0) sh_trailer2(trailer2, *unsup, verdict);
+  }
   const uint32_t i = (k0 + blockIdx.x) * SEG + threadIdx.x;
   const bool mine = i >= e0 && i < e1;
   uint32_t cls = 0, code = TB_CT_OK;
@@ -609,10 +636,10 @@ __global__ void __launch_bounds__(SEG) k_sh_reply(Dev d, Scratch s, WinDesc w, u
 // ------------------------------------------------------------------------------------------------
 __device__ inline bool sh_bit(const unsigned long long* bits, uint32_t i) { return (bits[i / 64] >> (i & 63)) & 1ull; }
 
-// Verdict of the window, identical on every shard: exchange 1's trailer (owners: duplicate id,
-// capacity, overflow bound) or exchange 2's (homes: an event outside the class).
-__device__ inline bool sh_abort(const uint32_t* trailer1, const uint32_t* trailer2) {
-  return (trailer1[0] | trailer1[1] | trailer1[2] | trailer2[0]) != 0;
+// Verdict of the window, identical on every shard: exchange 2's trailer (homes: an event outside the
+// class; owners: duplicate id, capacity, overflow bound).
+__device__ inline bool sh_abort(const uint32_t* trailer2) {
+  return (trailer2[0] | trailer2[1] | trailer2[2] | trailer2[3]) != 0;
 }
 
 // Per segment: committed owned-id entries (insert counts), over the segment lists.
@@ -630,21 +657,21 @@ __global__ void __launch_bounds__(SEG) k_sh_icount(Dev d, Scratch s, uint32_t xf
 
 template <bool XFER>
 __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w,
-                                                  const uint32_t* trailer1, const uint32_t* trailer2,
-                                                  const unsigned long long* bits, ChgLog chg, uint32_t chg_epoch) {
+                                                  const uint32_t* trailer2, const unsigned long long* bits,
+                                                  ChgLog chg, uint32_t chg_epoch) {
   __shared__ uint32_t lds[SEG / 64];
   __shared__ u128 ldsm[SEG / 64];
   // inserted transfer records, compacted per wave and stored as one contiguous run (as in k_final)
   __shared__ uint4 stage[XFER ? SEG * 8 : 1];
   Globals* g = d.g;
   const bool last_block = blockIdx.x == gridDim.x - 1;
-  if (sh_abort(trailer1, trailer2)) {
+  if (sh_abort(trailer2)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&g->window_error, 2u);
     if (last_block && threadIdx.x == 0) sh_window_reset(g, XFER, 0, false);
     return;
   }
-  const bool prefix_win = XFER && (g->win_flags & 2u) != 0;  // k_sh_close
-  const bool small = XFER && g->small_win != 0;              // k_sh_close
+  const bool prefix_win = XFER && (g->win_flags & 2u) != 0;  // sh_close_fold
+  const bool small = XFER && g->small_win != 0;              // sh_close_fold
   const uint64_t xbase = g->base;  // captured by k_sh_icount: the last block rewrites the count
   const uint32_t n = s.cnt_w[blockIdx.x];
   uint32_t i = 0, roles = 0;
