@@ -169,9 +169,9 @@ __host__ __device__ inline uint64_t xch2_bytes(uint32_t E) { return 16 + 8ull * 
 // stored id, owned ids reaching the exists check << 4.
 enum : uint32_t { SHX_HUGE = 1, SHX_DUP = 2, SHX_NONMONO = 4, SHX_FRESH = 8, SHX_OWN_SHIFT = 4 };
 
-// After exchange 1 (stream-ordered, one 1024-thread block: block 0 of k_sh_reply, or k_sh_close when
-// this shard is home to no event): folds the scan blocks' partials (no same-address atomics across
-// blocks) into this shard's window verdicts, returned to thread 0 as bit 0 (duplicate id or
+// After exchange 1 (stream-ordered, one 1024-thread block, red[] one entry per wave: block 0 of
+// k_sh_reply, or k_sh_close when this shard is home to no event): folds the scan blocks' partials
+// (no same-address atomics across blocks) into this shard's window verdicts, returned to thread 0 as bit 0 (duplicate id or
 // mismatch slots overflowed), bit 1 (capacity), bit 2 (overflow bound), and sets
 // Globals::win_flags bit 1 (the owned records extend the sorted prefix) and small_win for k_sh_apply.
 // The verdicts travel in exchange 2's trailer, so exchange 1 needs no fold before it.
@@ -193,9 +193,18 @@ __device__ inline uint32_t sh_close_fold(Dev d, const Scratch& s, uint32_t nblk,
   }
   if (a) atomicOr(bits_s, a);
   if (own) atomicAdd(own_s, own);
-  __syncthreads();  // (the LDS atomics above, before thread 0 reads them)
-  const u128 tot = xfer ? block_sum_u128(v, red) : (u128)0;
+  // the amounts: wave sums of the two 64-bit halves, one LDS word per wave, one barrier
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t lo = __shfl_xor((unsigned long long)(uint64_t)v, o, 64);
+    const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(v >> 64), o, 64);
+    v += ((u128)hi << 64) | lo;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();  // (also orders the LDS atomics above before thread 0 reads them)
   if (threadIdx.x != 0) return 0;
+  u128 tot = 0;
+  for (uint32_t w2 = 0; w2 < blockDim.x / 64; w2++) tot += red[w2];
   Globals* g = d.g;
   const uint32_t bits = *bits_s;
   uint32_t verdict = (bits & SHX_DUP) ? 1u : 0u;
@@ -226,7 +235,7 @@ __device__ inline void sh_trailer2(uint32_t* trailer2, uint32_t unsup, uint32_t 
 
 // A shard home to no event of the window still folds its owner verdicts into exchange 2.
 __global__ void __launch_bounds__(1024) k_sh_close(Dev d, Scratch s, uint32_t nblk, uint32_t xfer, uint32_t* trailer2) {
-  __shared__ u128 red[1024];
+  __shared__ u128 red[1024 / 64];
   __shared__ uint32_t bits_s;
   __shared__ unsigned long long own_s;
   const uint32_t verdict = sh_close_fold(d, s, nblk, xfer, red, &bits_s, &own_s);
@@ -591,7 +600,7 @@ __global__ void __launch_bounds__(SEG) k_sh_reply(Dev d, Scratch s, WinDesc w, u
                                                   const uint32_t* unsup, uint32_t* trailer2, uint32_t nscan,
                                                   uint32_t xfer) {
   __shared__ uint32_t lds[SEG / 64];
-  __shared__ u128 red[SEG];
+  __shared__ u128 red[SEG / 64];
   __shared__ uint32_t bits_s;
   __shared__ unsigned long long own_s;
   if (blockIdx.x == 0) {  // (block-uniform) exchange 2's trailer, instead of a memset before the homes
