@@ -78,7 +78,8 @@ int tbg_input_valid(const tbg_engine *engine, uint32_t operation, uint64_t input
 /* StateMachine.pulse (state_machine.zig:589-596): *needed = pulse_next_timestamp <= prepare_ts, with
  * the reference's exact pulse_next_timestamp (lowered by every timeout creation that ran ok, also in
  * a chain rolled back later; reset to timestamp_min by a post/void of the transfer whose expiry it
- * holds; set by each pulse's finish). Synchronizes. */
+ * holds; set by each pulse's finish). A host compare after a synchronous commit (which reads the value
+ * back with its reply); synchronizes only when windows were queued since. */
 int tbg_pulse_needed(tbg_engine *engine, uint64_t prepare_timestamp, int *needed);
 
 /* StateMachine.prefetch (state_machine.zig:598-648): stages the request on the device and resolves
@@ -143,6 +144,12 @@ int tbg_host_window_done(tbg_engine *engine, uint64_t ticket, int *done);
 /* Pinned host memory (hipHostMalloc) for message buffers the engine copies from / to. */
 int tbg_host_alloc(size_t bytes, void **out);
 int tbg_host_free(void *p);
+/* Page-locks a caller-owned host range in place (hipHostRegister), e.g. a replica's message pool
+ * (vsr/message_pool.zig allocates every message buffer once at startup): a tbg_prefetch / tbg_commit
+ * request inside a registered or tbg_host_alloc range reaches the device by one DMA, without the copy
+ * into the engine's staging buffer. The request must then stay unchanged until its commit returns. */
+int tbg_host_register(void *p, size_t bytes);
+int tbg_host_unregister(void *p);
 
 /* Waits for all work queued on the engine's stream. TBG_E_WINDOW (reported once) if a window was
  * rejected (see tbg_commit_window). */

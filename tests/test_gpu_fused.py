@@ -438,13 +438,13 @@ def test_sync_pending_commit_then_fused_only_windows_pulse():
 
 
 @pytest.mark.gpu
-def test_fused_resumes_after_overflow_bound_passes_2_63():
+def test_fused_overflow_bound_retightened_at_checkpoints():
     """Globals::ovf_bound sums every committed amount (it must bound every dp+dpo / cp+cpo without
-    reading them). Amounts just below the fused class's 2^43 cap, queued without syncs, drive it past
-    2^63 (~128 windows of 8192 events), where the fused pass stops (windows replayed through the
-    general path at sync). The next state read re-tightens it to the accounts' largest balance sum
-    (restore.h k_ovf_rescan, ~2^53 here), and the fused pass resumes. Replies and stores vs the
-    restatement throughout."""
+    reading them). Amounts just below the fused class's 2^43 cap add ~2^56 per 8192-event window, so
+    without re-tightening the bound would pass 2^63 after ~128 windows and the fused pass would stop.
+    The engine re-tightens it at a fixed point of the commit stream (every OVF_RESCAN_EVERY-th window,
+    restore.h k_ovf_rescan, gated on the device), never at a state read: 132 queued windows stay on the
+    fused pass, state reads run no rescan, and replies and stores match the restatement."""
     n_acc = 2000
     gpu, ref = _engines(n_acc, 1 << 21)
     try:
@@ -460,16 +460,18 @@ def test_fused_resumes_after_overflow_bound_passes_2_63():
                 ev["amount_lo"] = big - (ev["amount_lo"] % 4096)
             return b
 
+        st_start = gpu.stats()
         for w in range(132):
             b = win()
             outs.append((_queue(gpu, b), oracle_batches(ref, Operation.create_transfers, b)))
         gpu.sync()
         st0 = gpu.stats()
-        assert st0["fused_windows"] < 132  # the bound passed 2^63 inside the queue
+        assert st0["ovf_rescans"] >= 1  # the checkpoint inside the queue re-tightened the bound
+        assert st0["fused_windows"] - st_start["fused_windows"] == 132  # it never reached 2^63
         for h, r in outs:
             assert _replies(h) == r
-        # (the sync's state read on the drained stream already re-tightened the bound)
-        assert st0["ovf_rescans"] >= 1
+        for _ in range(4):  # state reads are not checkpoints
+            assert gpu.stats()["ovf_rescans"] == st0["ovf_rescans"]
         outs = []
         for w in range(6):
             b = win()
@@ -478,8 +480,7 @@ def test_fused_resumes_after_overflow_bound_passes_2_63():
             outs.append((h, oracle_batches(ref, Operation.create_transfers, b)))
         for h, r in outs:
             assert _replies(h) == r
-        st1 = gpu.stats()
-        assert st1["fused_windows"] >= st0["fused_windows"] + 3  # back on the fused pass
+        assert gpu.stats()["fused_windows"] == st0["fused_windows"] + 6
         _compare_final(gpu, ref)
     finally:
         gpu.close()

@@ -1,0 +1,111 @@
+"""The synchronous StateMachine path as a replica drives it (state_machine.zig:2719-2739 harness
+order: pulse() check, prefetch, commit per batch; vsr/replica.zig:3764-3772, 4149-4159): requests in a
+pinned message pool (tbg_host_alloc) or in caller memory page-locked in place (tbg_host_register)
+reach the device by one DMA, and pulse() compares against the host mirror of pulse_next that every
+commit reads back with its reply (include/tbg.h). Replies, every pulse() decision,
+pulse_next_timestamp and the final stores equal the restatement's."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from chaos import Chaos
+from oracle_sm import OracleStateMachine
+from test_gpu_parity import _compare_final
+from tigerbeetle_amd.types import NS_PER_S, Operation
+
+BM = 256
+_POOL = []  # pinned message pools live until the process ends (a failing assert's traceback may show them)
+
+
+def _pool(nbytes):
+    from tigerbeetle_amd.state_machine import HostBuffer
+
+    _POOL.append(HostBuffer(nbytes))
+    return _POOL[-1]
+
+
+def _step(sm, operation, body, tick):
+    """run_protocol (tests/chaos.py) over a request that is a uint8 array; returns (pulsed, reply)."""
+    sm.prepare_timestamp += tick + 1
+    sm.prepare(operation, body)
+    T = sm.prepare_timestamp
+    pulsed = sm.pulse()
+    if pulsed:
+        sm.prefetch_timestamp = T
+        sm.prefetch(1, Operation.pulse, b"")
+        sm.commit(0, 1, T, Operation.pulse, b"")
+    sm.prefetch_timestamp = T
+    sm.prefetch(2, operation, body)
+    return pulsed, sm.commit(0, 2, T, operation, body)
+
+
+def _stream(seed, n_batches):
+    ch = Chaos(seed, n_accounts=60, pending=0.35, linked=0.1, limits=0.2)
+    out = [(Operation.create_accounts, ch.accounts_batch(64), 0)]
+    for b in range(n_batches):
+        tick = NS_PER_S if b % 3 == 0 else (7 * NS_PER_S if b % 11 == 5 else 0)
+        out.append((Operation.create_transfers, ch.transfers_batch(BM), tick))
+    return out
+
+
+@pytest.mark.gpu
+def test_sync_pinned_message_pool_two_phase_chaos():
+    from tigerbeetle_amd import StateMachine
+
+    gpu = StateMachine(batch_max=BM, accounts_max=1024, transfers_max=1 << 15)
+    ref = OracleStateMachine(batch_max=BM)
+    pool = _pool(4 * BM * 128)  # a few message buffers, reused round-robin
+    pulses = 0
+    try:
+        for k, (op, ev, tick) in enumerate(_stream(3, 40)):
+            raw = np.frombuffer(ev.tobytes(), np.uint8)
+            slot = (k % 4) * BM * 128
+            body = pool.array[slot:slot + raw.size]
+            body[:] = raw
+            p1, r1 = _step(gpu, op, body, tick)
+            p2, r2 = _step(ref, op, raw.tobytes(), tick)
+            assert p1 == p2, k
+            assert r1 == r2, k
+            pulses += p1
+            assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp(), k
+        assert pulses >= 3
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_sync_registered_caller_buffer_and_unregistered_fallback():
+    """One page-aligned caller buffer registered in place and reused for every request, then the same
+    stream from pageable memory (the staging copy): identical replies."""
+    from tigerbeetle_amd import StateMachine, _lib
+
+    L = _lib.lib()
+    page = 4096
+    backing = np.zeros(BM * 128 + 2 * page, np.uint8)
+    _POOL.append(backing)  # (never freed while registered)
+    off = (-backing.ctypes.data) % page
+    buf = backing[off:off + BM * 128]
+    _lib.check(L.tbg_host_register(buf.ctypes.data, buf.size), "host_register")
+    engines = [StateMachine(batch_max=BM, accounts_max=1024, transfers_max=1 << 15) for _ in range(2)]
+    ref = OracleStateMachine(batch_max=BM)
+    try:
+        for k, (op, ev, tick) in enumerate(_stream(9, 24)):
+            raw = np.frombuffer(ev.tobytes(), np.uint8)
+            body = buf[:raw.size]
+            body[:] = raw
+            p_reg, r_reg = _step(engines[0], op, body, tick)
+            p_page, r_page = _step(engines[1], op, raw.tobytes(), tick)
+            p_ref, r_ref = _step(ref, op, raw.tobytes(), tick)
+            assert (p_reg, p_page) == (p_ref, p_ref), k
+            assert r_reg == r_ref, k
+            assert r_page == r_ref, k
+        for g in engines:
+            _compare_final(g, ref)
+    finally:
+        for g in engines:
+            g.close()
+        ref.close()
+        _lib.check(L.tbg_host_unregister(ctypes.c_void_p(buf.ctypes.data)), "host_unregister")

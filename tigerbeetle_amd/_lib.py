@@ -19,7 +19,8 @@ EXPORTS = [
     "tbg_shard_prepare_window", "tbg_shard_decide_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
     "tbg_shard_commit_bits_bytes", "tbg_window_changes", "tbg_windows_committed",
     "tbg_open", "tbg_reset", "tbg_prefetch_poll", "tbg_compact", "tbg_checkpoint", "tbg_digest",
-    "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free", "tbg_checksum",
+    "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free", "tbg_host_register",
+    "tbg_host_unregister", "tbg_checksum",
     "tbg_demux_init", "tbg_demux_decode", "tbg_aof_replay", "tbg_shard_gather_bytes", "tbg_shard_gather",
     "tbg_shard_gather_window_bytes", "tbg_shard_gather_window", "tbg_gathered_objects",
     "tbg_shard_apply", "tbg_open_device", "tbg_device_state", "tbg_device_history", "tbg_shard_lookup_bytes",
@@ -142,6 +143,8 @@ def lib():
         "tbg_host_window_done": ([vp, u64, P(ctypes.c_int)], i32),
         "tbg_host_alloc": ([ctypes.c_size_t, P(vp)], i32),
         "tbg_host_free": ([vp], i32),
+        "tbg_host_register": ([vp, ctypes.c_size_t], i32),
+        "tbg_host_unregister": ([vp], i32),
         "tbg_checksum": ([vp, vp, vp, u32, vp, vp], i32),
         "tbg_demux_init": ([P(Demuxer), u32, vp, u32], i32),
         "tbg_demux_decode": ([P(Demuxer), u32, u32, P(vp), P(u32)], i32),

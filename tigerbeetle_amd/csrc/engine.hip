@@ -30,6 +30,8 @@
 #include <cstddef>
 #include <new>
 #include <vector>
+#include <mutex>
+#include <utility>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -1672,7 +1674,9 @@ __global__ void k_setup(Dev d, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dp
   if (m > d.g->ovf_bound) d.g->ovf_bound = m;
 }
 
+#include "shard_gw.h"
 #include "host.inc"
 #include "aof.inc"
 #include "shard_gx.inc"
+#include "shard_gw.inc"
 #include "shard_read.inc"

@@ -95,14 +95,21 @@ __global__ void k_load_finish(Dev d, const LoadBound* lb, uint64_t n_acc, uint64
 // Re-tightening the overflow bound. Globals::ovf_bound only grows while windows commit (each adds its
 // amount sum: it must stay >= every dp+dpo and cp+cpo without reading them), so after enough volume
 // it is far above any real balance sum and the overflow-free fast paths (fused pass: below 2^63;
-// 64-bit no-return adds: below 2^64) would stay off for good. When the host sees it past
-// OVF_RESCAN_AT at a state read, one grid pass sets it to the accounts' largest sum again (the
+// 64-bit no-return adds: below 2^64) would stay off for good. The host launches this pair at a fixed
+// point of the commit stream (every OVF_RESCAN_EVERY-th window, host.inc ovf_checkpoint), so replicas
+// fed the same windows take the same paths; on the device both kernels return at once unless the bound
+// is past OVF_RESCAN_AT, and then one grid pass sets it to the accounts' largest sum again (the
 // LoadBound rule of open: exact while every sum fits 64 bits).
 // ------------------------------------------------------------------------------------------------
 #define OVF_RESCAN_AT ((u128)1 << 62)
+#define OVF_RESCAN_EVERY 64u
 
-__global__ void __launch_bounds__(256) k_ovf_rescan(Dev d, uint64_t n, LoadBound* lb) {
+__device__ inline bool ovf_rescan_due(const Globals* g) { return !g->window_error && g->ovf_bound >= OVF_RESCAN_AT; }
+
+__global__ void __launch_bounds__(256) k_ovf_rescan(Dev d, LoadBound* lb) {
   __shared__ unsigned long long lh[256 / 64], ll[256 / 64];
+  if (!ovf_rescan_due(d.g)) return;  // (uniform: every thread reads the same words)
+  const uint64_t n = d.g->acc_count;
   unsigned long long hi = 0, lo = 0;
   for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
     const tb_account_t& a = d.acc[k];
@@ -134,11 +141,12 @@ __global__ void __launch_bounds__(256) k_ovf_rescan(Dev d, uint64_t n, LoadBound
   }
 }
 
-__global__ void k_ovf_finish(Dev d, const LoadBound* lb) {
+__global__ void k_ovf_finish(Dev d, LoadBound* lb) {
   Globals* g = d.g;
-  if (g->window_error) return;  // (the host reads again after a reported or replayed window)
+  if (!ovf_rescan_due(g)) return;
   g->ovf_bound = lb->hi_max == ~0ull ? MAX128 : lb->hi_max ? (((u128)lb->hi_max << 64) | (u128)~0ull) : (u128)lb->lo_max;
   g->ovf_rescans++;
+  lb->hi_max = lb->lo_max = 0;  // (zero for the next checkpoint's pass)
 }
 
 // ------------------------------------------------------------------------------------------------

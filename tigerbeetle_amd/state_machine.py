@@ -27,6 +27,27 @@ def to_host(t):
     return c.numpy().copy()
 
 
+class HostBuffer:
+    """Pinned host memory from tbg_host_alloc, as a uint8 array: a replica's message buffer (allocated
+    once, vsr/message_pool.zig). A request in it reaches the device by one DMA (include/tbg.h
+    tbg_host_register)."""
+
+    def __init__(self, nbytes):
+        p = ctypes.c_void_p()
+        _lib.check(_lib.lib().tbg_host_alloc(nbytes, ctypes.byref(p)), "host_alloc")
+        self.ptr = p.value
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.ptr))
+
+    def close(self):
+        p, self.ptr = getattr(self, "ptr", None), None
+        if p and _lib is not None and _lib.lib is not None:
+            self.array = None
+            _lib.lib().tbg_host_free(p)
+
+    def __del__(self):
+        self.close()
+
+
 class StateMachine:
     def __init__(self, device=0, batch_max=BATCH_MAX, accounts_max=1 << 16, transfers_max=1 << 20,
                  window_events_max=0, resolver=True, components=True, shard_count=0, shard_index=0,
@@ -78,7 +99,7 @@ class StateMachine:
 
     def prefetch(self, op, operation, data):
         self._pf_data = data
-        self._pf = np.frombuffer(data, np.uint8) if data else np.zeros(0, np.uint8)
+        self._pf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(0, np.uint8)
         ptr = self._pf.ctypes.data if len(data) else None
         _lib.check(_lib.lib().tbg_prefetch(self.h, op, int(operation), ptr, len(data), self.prefetch_timestamp),
                    "prefetch")
@@ -86,9 +107,10 @@ class StateMachine:
     def commit(self, client, op, timestamp, operation, data):
         # the prefetched request (the same buffer, so tbg_commit finds its prefetch)
         pf = getattr(self, "_pf", None)
-        same = pf is not None and (data is self._pf_data or pf.tobytes() == data)
+        same = pf is not None and (data is self._pf_data or
+                                   np.array_equal(pf, np.frombuffer(data, np.uint8) if len(data) else pf[:0]))
         buf = pf if same else (
-            np.frombuffer(data, np.uint8) if data else np.zeros(0, np.uint8))
+            np.frombuffer(data, np.uint8) if len(data) else np.zeros(0, np.uint8))
         ptr = buf.ctypes.data if len(data) else None
         n = ctypes.c_uint64()
         _lib.check(_lib.lib().tbg_commit(self.h, op, timestamp, int(operation), ptr, len(data),

@@ -1,0 +1,62 @@
+#!/bin/bash
+# One parameterised driver for GPU-box runs (repo root, under gpurun). Each step runs under its own
+# time limit and the first failure ends the script. Results go to gpurun_out/$OUT (default r5/).
+#   tools/gpu.sh test [pytest -k expr]     the GPU suite (or a selection)
+#   tools/gpu.sh smoke                     __graft_entry__.smoke()
+#   tools/gpu.sh bench NAME [bench args]   one bench line -> bench_NAME.json (+ a one-line summary)
+#   tools/gpu.sh prof NAME [bench args]    rocprofv3 kernel trace + stats of one bench line, then one
+#                                          PMC pass per counter (FETCH_SIZE, WRITE_SIZE), summarised by
+#                                          tools/pmc_summary.py into pmc_NAME.json
+#   tools/gpu.sh rehearse NAME [args]      tools/rehearse_shards.py -> rehearse_NAME.json
+# Several commands chain with "+": tools/gpu.sh test + bench default + prof cfg2 --config cfg2
+set -o pipefail
+export TMPDIR=/tmp
+out=gpurun_out/${OUT:-r5}
+mkdir -p $out
+B="--no-cpu-baseline --host-fed-transfers 0 --sync-commit-batches 0"
+
+summary() {  # bench json -> value, roofline kernel avg launch, frac, sync line
+  python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d.get('roofline') or {};print(sys.argv[2],d['value'],r.get('avg_launch_us'),r.get('frac'),(d.get('sync_commit') or {}).get('value'))" "$1" "$2"
+}
+
+step() {
+  local cmd=$1; shift
+  case $cmd in
+    test)
+      local sel=()
+      [ -n "$1" ] && sel=(-k "$1")
+      timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${sel[@]}" \
+        > $out/pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|error" $out/pytest.log | head -20; tail -3 $out/pytest.log; return 1; }
+      tail -1 $out/pytest.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $out/smoke.log; return 1; }
+      tail -1 $out/smoke.log ;;
+    bench)
+      local name=$1; shift
+      timeout -k 10 400 python bench.py "$@" > $out/bench_$name.json 2> $out/bench_$name.err || { echo "bench $name failed"; tail -5 $out/bench_$name.err; return 1; }
+      summary $out/bench_$name.json $name ;;
+    prof)
+      local name=$1; shift
+      local d=$out/prof_$name
+      mkdir -p $d
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d/trace -o run -- python3 bench.py $B "$@" > $d/trace.log 2>&1 || { echo "trace $name failed"; tail -5 $d/trace.log; return 1; }
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/fetch -o run -- python3 bench.py $B "$@" --no-phase-timing > $d/fetch.log 2>&1 || { echo "fetch $name failed"; return 1; }
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/write -o run -- python3 bench.py $B "$@" --no-phase-timing > $d/write.log 2>&1 || { echo "write $name failed"; return 1; }
+      python tools/pmc_summary.py $d $out/pmc_$name.json && head -c 600 $out/pmc_$name.json; echo ;;
+    rehearse)
+      local name=$1; shift
+      timeout -k 10 600 python -u tools/rehearse_shards.py "$@" > $out/rehearse_$name.json 2> $out/rehearse_$name.err || { echo "rehearse $name failed"; tail -5 $out/rehearse_$name.err; return 1; }
+      tail -c 1500 $out/rehearse_$name.json ;;
+    *) echo "unknown step $cmd"; return 1 ;;
+  esac
+}
+
+args=()
+for a in "$@" +; do
+  if [ "$a" = "+" ]; then
+    [ ${#args[@]} -gt 0 ] && { step "${args[@]}" || exit 1; }
+    args=()
+  else
+    args+=("$a")
+  fi
+done
