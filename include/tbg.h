@@ -296,26 +296,44 @@ int tbg_aof_replay(tbg_engine *engine, const void *h_aof, uint64_t size, uint32_
 uint64_t tbg_shard_gather_bytes(uint32_t n_events, uint32_t shard_count, uint32_t batch_max, uint64_t *phase2_offset);
 int tbg_shard_gather(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_events,
                      uint64_t timestamp, uint32_t phase, void *d_buffer);
-/* The general class a whole window at a time (replaces one gather round per batch): phase 1 gathers
- * the accounts and stored transfers every event of the window names and EVERY live entry due at or
- * before t_last (the window's last batch timestamp), up to due_cap per shard (the shard's count in the
- * buffer's first bytes: uint32 word shard_index, 0xFFFFFFFF when it had more: the window then goes
- * batch by batch), plus each shard's smallest live entry beyond t_last; phase 2 the accounts of the
- * gathered pending and due transfers. Asynchronous, no host round trip. After both sums,
- * tbg_gathered_objects writes the distinct gathered objects in timestamp order (sorted and
- * deduplicated on the device on the timestamp bits below t_last's, so on the engine that ran this
- * window's phase 1; synchronous: the counts size the scratch engine's tbg_open_device),
- * the scratch engine commits the whole window (tbg_commit_window: the pulses inside it modelled as on
- * one engine, or TBG_E_WINDOW at tbg_sync, then nothing is applied and the window goes batch by
- * batch), and tbg_shard_apply keeps the owned objects. Replaces tbg_shard_gather per batch; the
- * same buffer rules (256-byte aligned, one writer per slot). */
-uint64_t tbg_shard_gather_window_bytes(uint32_t n_events, uint32_t shard_count, uint32_t due_cap,
-                                       uint64_t *phase2_offset);
-int tbg_shard_gather_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_events,
-                            uint64_t t_last, uint32_t phase, void *d_buffer, uint32_t due_cap);
-int tbg_gathered_objects(tbg_engine *engine, const void *d_buffer, uint32_t n_events, uint32_t due_cap,
-                         void *d_accounts, uint64_t *n_accounts, void *d_transfers, uint8_t *d_status,
-                         uint64_t *n_transfers);
+/* The general class a whole window at a time (tigerbeetle_amd/csrc/shard_gw.inc; replaces one gather
+ * round per batch). Every shard lists the objects it owns of the window's read set, each once (phase 1:
+ * the accounts and stored transfers the events name, every live entry due at or before t_last — the
+ * window's last batch timestamp — and the smallest live entry beyond it; phase 2: the accounts of the
+ * phase-1 transfers), and the lists are concatenated across the shards by sums:
+ *   tbg_gw_collect(phase): this shard's counts into its words of d_counts (16 x G bytes, the rest
+ *     zeroed); sum d_counts across the shards;
+ *   tbg_gw_write(phase): (synchronous: reads the summed counts) zero-fills the regions and writes this
+ *     shard's records at its offset: phase 1 accounts [0, a1) of d_accounts and transfers [0, x1) of
+ *     d_transfers / d_status (*n_accounts = a1, *n_transfers = x1), phase 2 accounts [a1, a1 + a2)
+ *     (*n_accounts = a2); sum those regions. *overflow = 1 (phase 1) when a shard had more than due_cap
+ *     entries due: nothing written, commit the window batch by batch (tbg_shard_gather);
+ *   tbg_gw_commit: the scratch engine `scratch` (an unsharded engine of this process whose
+ *     accounts_max records fit d_accounts: its account store is bound to it) keeps the acc_base
+ *     accounts it held after the previous general window (0: it starts over; then tbg_gw_collect must
+ *     have been called with restart = 1, and the accounts are gathered at d_accounts + acc_base),
+ *     takes the gathered records (transfers sorted by timestamp) with no host round trip, commits the
+ *     window (tbg_commit_window semantics, replies into d_results / d_batch_base), and this shard
+ *     applies its part (every scratch account it owns that changed, its gathered transfers' statuses,
+ *     the new records it owns, its pulse_next_timestamp). Asynchronous. The scratch may be kept only
+ *     while nothing but general windows commits on the shards: restart after any other commit, pulse or
+ *     open;
+ *   tbg_gw_result: waits; *rejected = 1 when the scratch engine rejected the window (a pulse inside it
+ *     reaching the expiry cap, or one falling due in a window that reads balances): nothing was applied
+ *     on the shard, commit it batch by batch (and restart the scratch). *scratch_accounts: the
+ *     next window's acc_base. TBG_E_CAPACITY when this shard's stores could not take its new records
+ *     (nothing applied on it). */
+int tbg_gw_collect(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_events, uint64_t t_last,
+                   uint32_t phase, uint32_t due_cap, const void *d_gathered_transfers, uint32_t n_gathered_transfers,
+                   void *d_counts, int restart);
+int tbg_gw_write(tbg_engine *engine, uint32_t phase, const void *d_counts, void *d_accounts, uint64_t accounts_cap,
+                 void *d_transfers, uint8_t *d_status, uint64_t transfers_cap, uint32_t *n_accounts,
+                 uint32_t *n_transfers, int *overflow);
+int tbg_gw_commit(tbg_engine *engine, tbg_engine *scratch, uint32_t operation, const void *d_events,
+                  uint32_t n_batches, const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_accounts,
+                  uint64_t acc_base, const void *d_transfers, const uint8_t *d_status, void *d_results,
+                  uint32_t *d_batch_base, int auto_pulse, uint64_t prepare_timestamp);
+int tbg_gw_result(tbg_engine *engine, tbg_engine *scratch, int *rejected, uint64_t *scratch_accounts);
 /* d_history / d_history_side (tbg_device_history of the scratch engine, may be NULL): the history
  * row beside each of d_transfers, kept with the transfers this shard inserts. With
  * TBG_FLAG_CHANGE_LOG the shard's write-back stream (tbg_window_changes) then lists what changed on

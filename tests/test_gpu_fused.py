@@ -113,7 +113,7 @@ def test_fused_matches_oracle_with_static_failures_and_retries():
         ref.close()
 
 
-OUT_OF_CLASS = ["pending", "linked", "limit", "history", "order", "huge", "balancing", "post"]
+OUT_OF_CLASS = ["void", "linked", "limit", "history", "order", "huge", "balancing", "post"]
 
 
 @pytest.mark.gpu
@@ -137,9 +137,10 @@ def test_fused_speculation_undone(kind, where):
         first += WIN * BM
         b, j = (0, 3) if where == "first" else (WIN - 1, BM - 5)
         ev = batches[b]
-        if kind == "pending":
-            ev["flags"][j] = 2
-            ev["timeout"][j] = 30
+        if kind == "void":
+            ev["flags"][j] = 8
+            ev["pending_id_lo"][j] = 17
+            ev["amount_lo"][j] = 0
         elif kind == "linked":
             ev["flags"][j] = 1
         elif kind == "limit":
@@ -539,9 +540,11 @@ def test_fused_claim_mode_ids_that_do_not_rise(order):
 @pytest.mark.gpu
 def test_sync_prefetch_commit_runs_the_fused_pass():
     """The synchronous StateMachine calls (pulse() check, prefetch, commit per batch: a replica that
-    does not pipeline): order-free batches commit through the fused pass (the prefetch only stages
-    the request), batches outside the class (pending with timeouts, limits, chains) are replayed
-    through the general path inside the same commit; replies and stores equal the restatement's."""
+    does not pipeline): order-free batches, pending ones with timeouts included, commit through the
+    fused pass (the prefetch only stages the request); batches outside the class (a limit account,
+    chains, posts/voids of earlier pending transfers) all through the stream are replayed through the
+    general path inside the same commit, and the speculation's back-off (capped at 8 batches) leaves
+    most clean batches on the fused pass. Replies and stores equal the restatement's."""
     from chaos import run_protocol
 
     n_acc = 2000
@@ -549,24 +552,80 @@ def test_sync_prefetch_commit_runs_the_fused_pass():
     try:
         _accounts(gpu, ref, n_acc + 2, flags={n_acc: 2})
         first = 0
-        for b in range(24):
+        clean = 0
+        for b in range(48):
             ev = workload.transfers_uniform(first, BM, seed=41, n_accounts=n_acc)
             first += BM
-            # batches outside the class (pending with timeouts, a limit account, chains) in the first
-            # half only: each backs the speculation off for 2^fails batches (1 + 2 + 4 + 8 here), so
-            # most of the clean second half runs fused again
-            if b < 12 and b % 6 == 2:
-                ev["flags"][::37] = 2
+            if b % 8 == 1:
+                ev["flags"][::37] = 2  # pending, in the class
                 ev["timeout"][::37] = 1
-            elif b < 12 and b % 6 == 4:
+            elif b % 8 == 4:
                 ev["debit_account_id_lo"][5] = n_acc + 1  # the account with a limit flag
-            elif b < 12 and b % 6 == 5:
-                ev["flags"][10:14] = 1
-            tick = 2 * 10**9 if b % 6 == 3 else 0
+            elif b % 8 == 5:
+                ev["flags"][10:14] = 1  # a chain
+            elif b % 8 == 7:
+                ev["flags"][20] = 4  # post of an earlier pending transfer
+                ev["pending_id_lo"][20] = ev["id_lo"][0] - 6 * BM
+                ev["amount_lo"][20] = 0
+            clean += int(b % 8 not in (4, 5, 7))
+            tick = 2 * 10**9 if b % 8 == 3 else 0
             assert run_protocol(gpu, Operation.create_transfers, ev, tick) == \
                 run_protocol(ref, Operation.create_transfers, ev, tick), b
-        assert gpu.stats()["fused_windows"] >= 8
+        assert gpu.stats()["fused_windows"] >= clean // 2, (gpu.stats()["fused_windows"], clean)
         assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["sequential", "random"])
+def test_fused_pending_creates_in_class(order):
+    """About 1 % pending creates (half of them with 1-3 s timeouts) in order-free windows stay on the
+    fused pass: debits/credits_pending, the TransferPending rows, pulse_next_timestamp lowered to the
+    earliest expiry, live expiry entries. Later windows (a 4 s tick: the harness pulse expires them;
+    posts and voids of some on the general path) and the final stores equal the restatement's."""
+    n_acc = 2000
+    gpu, ref = _engines(n_acc, 1 << 20)
+    code = workload.ID_ORDERS[order]
+    rng = np.random.default_rng(9)
+    try:
+        _accounts(gpu, ref, n_acc)
+        first, pend_ids = 0, []
+        st0 = gpu.stats()
+        for w in range(5):
+            b = _window(first, n_acc)
+            first += WIN * BM
+            if code:  # transfer ids that do not rise (claim mode); the accounts stay
+                for ev in b:
+                    ev["id_lo"], ev["id_hi"] = workload.encode_ids(ev["id_lo"], code, 3)
+            for ev in b:
+                k = rng.choice(BM, size=10, replace=False)
+                ev["flags"][k] = 2
+                ev["timeout"][k[:5]] = rng.integers(1, 4, size=5)
+                pend_ids += list(zip(ev["id_lo"][k], ev["id_hi"][k]))
+            _check(gpu, ref, b)
+            assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
+        assert gpu.stats()["fused_windows"] - st0["fused_windows"] == 5
+        # posts / voids of some of them (general path), then a tick: the harness pulse expires the rest
+        pv = _window(first, n_acc)
+        first += WIN * BM
+        for j, ev in enumerate(pv[:2]):
+            for q in range(8):
+                lo, hi = pend_ids[j * 8 + q]
+                ev["flags"][q] = 4 if q % 2 == 0 else 8
+                ev["pending_id_lo"][q], ev["pending_id_hi"][q] = lo, hi
+                ev["amount_lo"][q] = 0
+        _check(gpu, ref, pv)
+        gpu.prepare_timestamp += 4 * 10**9
+        ref.prepare_timestamp += 4 * 10**9
+        for w in range(2):
+            b = _window(first, n_acc)
+            first += WIN * BM
+            _check(gpu, ref, b)
+        assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
+        assert (ref.dump_transfer_status() == 4).sum() > 0
         _compare_final(gpu, ref)
     finally:
         gpu.close()

@@ -282,3 +282,93 @@ def test_shard_cfg4_shape(G, win):
     finally:
         sh.close()
         ref.close()
+
+
+def _fallbacks(sh):
+    return {k: sum(s.gw_fallbacks[k] for s in sh.shards) for k in ("due_overflow", "rejected")}
+
+
+@pytest.mark.gpu
+def test_shard_general_window_due_overflow_falls_back():
+    """A shard with more entries due in a window's span than due_cap (here 3): the window path is
+    abandoned after phase 1's counts (nothing written) and the window goes batch by batch, each pulse
+    selecting among every shard's cap + 1 smallest. Replies, pulse_next_timestamp after every window,
+    and the union of the stores and statuses equal the restatement's."""
+    G, bm, win = 3, 16, 4
+    sh = LocalShards(G, bm, 2048, 1 << 14, win * bm, general="window")
+    for s in sh.shards:
+        s.due_cap = 3
+    ref = OracleStateMachine(batch_max=bm)
+    ch = Chaos(7400, n_accounts=12, pending=0.8, postvoid=0.1, limits=0.0, balancing=0.0, linked=0.05, invalid=0.0)
+    ref_log = []
+    try:
+        for w in range(14):
+            op = Operation.create_accounts if w < 1 else Operation.create_transfers
+            batches = [ch.accounts_batch(bm) if w < 1 else ch.transfers_batch(bm) for _ in range(win)]
+            tick = 0 if w < 2 else 3 * NS_PER_S
+            g, _ = sh.commit_any(op, batches, tick)
+            assert g == oracle_logged(ref, op, batches, tick, ref_log), f"window {w}"
+            assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp(), f"window {w}"
+        _check(sh, ref)
+        assert _fallbacks(sh)["due_overflow"] > 0
+        assert (ref.dump_transfer_status() == 4).sum() > 0
+    finally:
+        sh.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_shard_general_window_rejected_by_scratch_falls_back():
+    """Windows that read balances (limit flags on most accounts) with pulses due inside them (a tick
+    before every batch, 1-9 s timeouts): the scratch engine rejects them after modelling nothing
+    (TBG_E_WINDOW, the apply kernels check its verdict on the device), no shard applies anything, and
+    the window goes batch by batch. Stores, statuses and pulse_next_timestamp after every window equal
+    the restatement's."""
+    G, bm, win = 2, 16, 4
+    sh = LocalShards(G, bm, 2048, 1 << 14, win * bm, general="window")
+    ref = OracleStateMachine(batch_max=bm)
+    ch = Chaos(7500, n_accounts=16, pending=0.5, postvoid=0.2, limits=0.7, balancing=0.1, linked=0.1)
+    try:
+        for w in range(16):
+            op = Operation.create_accounts if w < 1 else Operation.create_transfers
+            batches = [ch.accounts_batch(bm) if w < 1 else ch.transfers_batch(bm) for _ in range(win)]
+            ticks = [0] * win if w < 1 else [NS_PER_S] * win
+            g, _ = sh.commit_any(op, batches, ticks=ticks)
+            assert g == [run_protocol(ref, op, ev, t) for ev, t in zip(batches, ticks)], f"window {w}"
+            assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp(), f"window {w}"
+        _check(sh, ref)
+        assert _fallbacks(sh)["rejected"] > 0
+    finally:
+        sh.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_shard_general_window_large_read_set():
+    """A window of 4 x 4096 events (more than one workgroup's worth of new records: the apply's
+    device-wide scan) whose read set spans most of 20000 accounts, two-phase and limits mixed in,
+    at G = 2 and 8 against the restatement."""
+    bm, win = 4096, 4
+    for G in (2, 8):
+        sh = LocalShards(G, bm, 32768, 1 << 17, win * bm, general="window")
+        ref = OracleStateMachine(batch_max=bm)
+        try:
+            acc = workload.accounts(0, 20000, seed=48)
+            for k in range(0, 20000, bm):
+                ev = acc[k:k + bm]
+                g, _ = sh.commit_any(Operation.create_accounts, [ev], 0)
+                assert g == [run_protocol(ref, Operation.create_accounts, ev, 0)]
+            xf = workload.transfers_cfg4(0, 3 * win * bm, 48, 20000, bm)
+            for w in range(3):
+                batches = [xf[(w * win + k) * bm:(w * win + k + 1) * bm] for k in range(win)]
+                ticks = [NS_PER_S] * win
+                g, took_fast = sh.commit_any(Operation.create_transfers, batches, ticks=ticks)
+                assert not took_fast
+                assert g == [run_protocol(ref, Operation.create_transfers, ev, t) for ev, t in zip(batches, ticks)], w
+                assert sh.shards[0].pulse_next() == ref.pulse_next_timestamp()
+            assert max(s._gw_n[0] for s in sh.shards) > 8192
+            _check(sh, ref)
+            assert _fallbacks(sh) == {"due_overflow": 0, "rejected": 0}
+        finally:
+            sh.close()
+            ref.close()

@@ -22,7 +22,7 @@ EXPORTS = [
     "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free", "tbg_host_register",
     "tbg_host_unregister", "tbg_checksum",
     "tbg_demux_init", "tbg_demux_decode", "tbg_aof_replay", "tbg_shard_gather_bytes", "tbg_shard_gather",
-    "tbg_shard_gather_window_bytes", "tbg_shard_gather_window", "tbg_gathered_objects",
+    "tbg_gw_collect", "tbg_gw_write", "tbg_gw_commit", "tbg_gw_result",
     "tbg_shard_apply", "tbg_open_device", "tbg_device_state", "tbg_device_history", "tbg_shard_lookup_bytes",
     "tbg_shard_lookup", "tbg_shard_lookup_reply", "tbg_shard_query_bytes", "tbg_shard_query", "tbg_shard_query_merge",
 ]
@@ -151,9 +151,10 @@ def lib():
         "tbg_aof_replay": ([vp, vp, u64, u32, P(AofStats)], i32),
         "tbg_shard_gather_bytes": ([u32, u32, u32, P(u64)], u64),
         "tbg_shard_gather": ([vp, u32, vp, u32, u64, u32, vp], i32),
-        "tbg_shard_gather_window_bytes": ([u32, u32, u32, P(u64)], u64),
-        "tbg_shard_gather_window": ([vp, u32, vp, u32, u64, u32, vp, u32], i32),
-        "tbg_gathered_objects": ([vp, vp, u32, u32, vp, P(u64), vp, vp, P(u64)], i32),
+        "tbg_gw_collect": ([vp, u32, vp, u32, u64, u32, u32, vp, u32, vp, ctypes.c_int], i32),
+        "tbg_gw_write": ([vp, u32, vp, vp, u64, vp, vp, u64, P(u32), P(u32), P(ctypes.c_int)], i32),
+        "tbg_gw_commit": ([vp, vp, u32, vp, u32, vp, vp, vp, u64, vp, vp, vp, vp, ctypes.c_int, u64], i32),
+        "tbg_gw_result": ([vp, vp, P(ctypes.c_int), P(u64)], i32),
         "tbg_shard_apply": ([vp, vp, u64, vp, vp, u64, vp, vp, u64], i32),
         "tbg_device_history": ([vp, P(vp), P(vp)], i32),
         "tbg_shard_lookup_bytes": ([u32], u64),

@@ -12,13 +12,19 @@
 // for the ranks measured 50 us per 1M-event window of blocks idling behind slower predecessors.
 //
 // Simple = every event of the window is either decided statically (validation, lookups, ledgers,
-// exists) or is a plain create (no linked / pending / post / void / balancing flag) whose accounts
-// carry no limit and no history flag, the ids are strictly increasing over the window in u128 order
+// exists) or is a create (single-phase, or pending with or without a timeout; no linked / post / void /
+// balancing flag) whose accounts carry no limit and no history flag, the ids are strictly increasing over the window in u128 order
 // (64-bit sequences and the reference's time-based 128-bit ids alike, docs/develop/data-modeling.md:
 // 186-203; so no id repeats: the window is claim-free), and every amount reaching the account checks is below
 // 2^43 with the overflow bound below 2^63 (so no balance field leaves its low 64-bit word: the
 // overflow checks of :1532-1545 cannot fail, and the balance adds are exact no-return 64-bit adds).
-// Then every outcome is a function of the pre-window state and the event alone.
+// Then every outcome is a function of the pre-window state and the event alone. A
+// pending create (round 5) adds to debits_pending / credits_pending instead of the posted fields
+// (:1555-1566), inserts its TransferPending row as pending, lowers pulse_next_timestamp to its expiry
+// when it has a timeout (:1576-1581: the last block folds the window's minimum) and gets a live entry
+// in the expires_at list (k_fu_final, once the window commits). None of it is read by another event
+// of an order-free window: no post/void is in the class, and the window's own timeouts fall due after
+// it (a window reaches the fused pass only if it spans less than a second).
 //
 // Speculation. Each block applies its balance adds as soon as its own events are simple; whether the
 // whole window is simple is known after the launch (Globals::fu_abort = this window's epoch when a
@@ -32,6 +38,7 @@
 
 #define FU_T 256
 #define FU_AMOUNT_MAX (1ull << 43)  // per-event amount bound: 2^20 events x 2^43 <= 2^63
+#define FU_BACKOFF_MAX 8u           // transfer windows the speculation waits at most after a miss
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
@@ -54,7 +61,8 @@ struct FuEv {
   uint32_t code, dr, cr;
   unsigned long long amount;  // C_REACH events: the amount (every one counts toward the overflow bound)
   u128 id_key;                // C_REACH events: the id (x_id_max bound)
-  bool simple, reach;
+  uint64_t expires_at;        // a pending create with a timeout: its expiry (0 = none)
+  bool simple, reach, pending;
 };
 
 // Claim mode (windows whose ids are not known to rise: Globals::mono_prev = 0): the ids that reach
@@ -83,8 +91,9 @@ __device__ __forceinline__ bool fu_claim(BEntry* bm, uint32_t mask, const uint8_
   }
 }
 
-// prev_id: the id of event i - 1 (i > 0). claim: claim mode (bm, bmask, tag), else the ids must rise.
-__device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id, const tb_transfer_t& t,
+// prev_id: the id of event i - 1 (i > 0). ts: the event's timestamp (the record as inserted). claim:
+// claim mode (bm, bmask, tag), else the ids must rise.
+__device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id, const tb_transfer_t& t, uint64_t ts,
                                           u128 x_id_max, uint64_t P, FuEv* o, bool claim = false,
                                           BEntry* bm = nullptr, uint32_t bmask = 0, const uint8_t* evb = nullptr,
                                           uint32_t tag = 0) {
@@ -92,7 +101,9 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
   o->dr = o->cr = NONE32;
   o->amount = 0;
   o->id_key = 0;
+  o->expires_at = 0;
   o->reach = false;
+  o->pending = (f & TB_TRANSFER_PENDING) != 0;
   // no chain, no post/void; claim-free (ids strictly increasing over the window, k_ct_prep's test)
   // unless in claim mode
   bool simple = !(f & TB_TRANSFER_LINKED) && !(f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
@@ -103,7 +114,7 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
   } else {
     code = ct_head(t);
     if (code == CONT) {
-      if (f & (TB_TRANSFER_PENDING | TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING | TB_TRANSFER_BALANCING_DEBIT |
+      if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING | TB_TRANSFER_BALANCING_DEBIT |
                TB_TRANSFER_BALANCING_CREDIT)) {
         simple = false;
       } else {
@@ -141,8 +152,16 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
             if (dup) simple = false;  // in-window duplicate
             uint32_t xs = mx ? x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id) : NONE32;
             if (xs == NONE32 && mx) xs = x_prefix_find(d.xr, P, t.id);
-            // :1506-1507; a plain create with timeout 0 cannot overflow the timeout (:1543)
+            // :1506-1507; then the balance tail (:1509-1547): its overflow checks cannot fail here (the
+            // amounts and the bound, above), the timeout's can (a single-phase create has timeout 0)
             code = xs != NONE32 ? ct_exists(t, d.xr[xs]) : (uint32_t)TB_CT_OK;
+            if (code == TB_CT_OK && t.timeout != 0) {
+              const uint64_t tns = (uint64_t)t.timeout * TB_NS_PER_S;
+              if (ovf64(ts, tns))
+                code = TB_CT_OVERFLOWS_TIMEOUT;
+              else
+                o->expires_at = ts + tns;
+            }
           }
         }
       }
@@ -159,7 +178,18 @@ struct FuScratch {
   u128* idmax;              // per block: its largest reaching id
   uint8_t* applied;         // per block: its balance adds were applied (k_fu_final undoes them)
   unsigned long long* ok;   // per wave: ok-event bitmap
+  unsigned long long* pend; // per wave: ok pending creates
+  unsigned long long* pto;  // per wave: ok pending creates with a timeout the expiry scan can see
+  unsigned long long* pnmin;  // per block: smallest expiry of its ok creates with a timeout (~0: none)
 };
+
+// The balance fields a create adds to: posted, or pending for a pending transfer (:1555-1566).
+__device__ __forceinline__ unsigned long long* fu_dr_field(const Dev& d, const FuEv& fe) {
+  return reinterpret_cast<unsigned long long*>(fe.pending ? &d.acc[fe.dr].debits_pending : &d.acc[fe.dr].debits_posted);
+}
+__device__ __forceinline__ unsigned long long* fu_cr_field(const Dev& d, const FuEv& fe) {
+  return reinterpret_cast<unsigned long long*>(fe.pending ? &d.acc[fe.cr].credits_pending : &d.acc[fe.cr].credits_posted);
+}
 
 __device__ __forceinline__ void fu_store_records(Dev d, const uint4* src, bool ok, unsigned long long okm,
                                                  uint64_t first_slot, uint4* ws) {
@@ -188,12 +218,14 @@ __device__ __forceinline__ void fu_store_records(Dev d, const uint4* src, bool o
 // Decide, apply, store in place. Writes nothing but scratch, the in-place records and statuses (slots
 // at or beyond the store's end) and, when its events are simple, the balance adds.
 __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
-                                                   WinDesc w, uint32_t epoch, uint32_t fo_only, uint32_t* fmark) {
+                                                   WinDesc w, uint32_t epoch, uint32_t fo_only, uint32_t* fmark,
+                                                   uint32_t pn_skip) {
   __shared__ uint4 stage[FU_T * 4];  // half of each inserted record per round (16 KiB)
   __shared__ uint32_t lds[FU_T / 64];
   __shared__ unsigned long long ldsu[FU_T / 64];
   __shared__ u128 ldsm[FU_T / 64];
   __shared__ uint32_t ldsn[FU_T / 64];
+  __shared__ unsigned long long ldsp[FU_T / 64];
   Globals* g = d.g;
   if (WIN_REJECTED(g)) return;
   const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -215,7 +247,11 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   const u128 x_id_max = g->x_id_max;
   const u128 ovf = g->ovf_bound;
   // window-level condition: the balance fields stay below 2^64 (ovf + 2^20 x 2^43 < 2^64)
-  const bool glob_ok = (uint64_t)(ovf >> 64) == 0 && (uint64_t)ovf < (1ull << 63) && !g->batch_huge;
+  // pn_skip: the host launched no pulse before this window (pulse_next was "never" at its last read);
+  // an earlier fused window may have lowered it since (a pending create with a timeout): if a pulse
+  // could be due before or inside this window, it leaves the class (replayed with its pulse)
+  const bool glob_ok = (uint64_t)(ovf >> 64) == 0 && (uint64_t)ovf < (1ull << 63) && !g->batch_huge &&
+                       !(pn_skip && g->pulse_next <= w.T[w.nb - 1]);
   // claim mode: the previous transfer window's ids did not rise (e.g. random ids): in-window
   // duplicates are found by claims instead of by the rising-id test
   const bool claim = g->mono_prev == 0;
@@ -269,11 +305,14 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
     if (lane == 0 && i > 0 && i < E) prev = U(ev[i - 1].id);
   }
   bool nonmono = false;  // (claim mode: whether the ids rise after all, for the next window)
+  fe.pending = false;
+  fe.expires_at = 0;
   if (i < E && !aborted) {
-    fu_decide(d, i, prev, t, x_id_max, P, &fe, claim, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev),
+    const uint64_t ts = win_ts(w, win_batch(w, i), i);  // :1253 (the record as inserted)
+    fu_decide(d, i, prev, t, ts, x_id_max, P, &fe, claim, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev),
               FU_CLAIM | epoch);
     nonmono = i > 0 && !(U(t.id) > prev);
-    t.timestamp = win_ts(w, win_batch(w, i), i);  // :1253 (the record as inserted)
+    t.timestamp = ts;
   }
   const bool blk_simple = __syncthreads_and(fe.simple && !aborted) && glob_ok;
   if (threadIdx.x == 0) {
@@ -285,8 +324,8 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   const bool ok = i < E && fe.code == TB_CT_OK;
   if (ok) {
     // no-return 64-bit adds: every field stays below 2^64 this window (glob_ok, FU_AMOUNT_MAX)
-    (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.dr].debits_posted), fe.amount);
-    (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.cr].credits_posted), fe.amount);
+    (void)atomicAdd(fu_dr_field(d, fe), fe.amount);
+    (void)atomicAdd(fu_cr_field(d, fe), fe.amount);
     if (fmark) {
       // write-back stream (changes.h): the accounts this window changed, tagged with its number;
       // counted only if the pass commits the window (k_chg_count)
@@ -297,8 +336,15 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   const bool bad = i < E && !ok;
   if (bad) s.code[i] = fe.code;
   const unsigned long long okm = __ballot(ok);
-  if (lane == 0 && i < E) fs.ok[i >> 6] = okm;
-  if (ok) d.xstatus[base + i] = 0;
+  // a pending create's live expiry entry needs a timestamp the expiry scan can see (composite key)
+  const bool pto = ok && fe.expires_at != 0 && !(t.timestamp >> 63) && fe.expires_at <= TB_TIMESTAMP_MAX;
+  const unsigned long long pendm = __ballot(ok && fe.pending), ptom = __ballot(pto);
+  if (lane == 0 && i < E) {
+    fs.ok[i >> 6] = okm;
+    fs.pend[i >> 6] = pendm;
+    fs.pto[i >> 6] = ptom;
+  }
+  if (ok) d.xstatus[base + i] = fe.pending ? (uint8_t)TB_PENDING_PENDING : (uint8_t)0;
   if (okm) {  // in place: slot base + i
     const uint32_t first = (uint32_t)__builtin_ctzll(okm);
     fu_store_records(d, reinterpret_cast<const uint4*>(&t), ok, okm, base + (i - lane) + first, stage + wave * 256);
@@ -308,16 +354,24 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   const unsigned long long wsum = wave_sum_u64(fe.reach ? fe.amount : 0ull);
   const u128 wmax = wave_max_u128(fe.reach ? fe.id_key : (u128)0);
   const bool wnm = __ballot(nonmono) != 0;
+  // pulse_next (:1576-1581): every ok create with a timeout, visible to the scan or not
+  unsigned long long pmin = ok && fe.expires_at ? fe.expires_at : ~0ull;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(pmin, o, 64);
+    pmin = y < pmin ? y : pmin;
+  }
   if (lane == 0) {
     lds[wave] = wbad;
     ldsu[wave] = wsum;
     ldsm[wave] = wmax;
     ldsn[wave] = wnm ? 1u : 0u;
+    ldsp[wave] = pmin;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t nbad = 0, nm = 0;
-    unsigned long long bsum = 0;
+    unsigned long long bsum = 0, bpmin = ~0ull;
     u128 bmax = 0;
 #pragma unroll
     for (uint32_t q = 0; q < FU_T / 64; q++) {
@@ -325,8 +379,10 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
       bsum += ldsu[q];
       bmax = umax128(bmax, ldsm[q]);
       nm |= ldsn[q];
+      bpmin = ldsp[q] < bpmin ? ldsp[q] : bpmin;
     }
     fs.cnt[k] = nbad;
+    fs.pnmin[k] = bpmin;
     // (claim mode) this block's ids do not rise: the window is hashed, and the next one claims too
     if (nm) __hip_atomic_store(&g->fu_nonmono, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     fs.pay[k] = bsum;
@@ -359,6 +415,7 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
   __shared__ uint32_t lds[FU_T / 64];
   __shared__ unsigned long long red[FU_T / 64];
   __shared__ u128 redm[FU_T / 64];
+  __shared__ unsigned long long redp[FU_T / 64];
   Globals* g = d.g;
   // (bit 0 only: this kernel itself may set bit 3, and every block must still undo its adds)
   if ((g->window_error & 1u) || g->fu_epoch != epoch) return;  // (k_ct_fused backed off or skipped)
@@ -369,7 +426,9 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
       g->sp_done = 0;
       const uint32_t fails = g->sp_fails + 1;
       g->sp_fails = fails;
-      g->sp_skip = fails >= 12 ? 4096u : (1u << fails);
+      // back-off capped at FU_BACKOFF_MAX windows: a stream that leaves the class now and then keeps
+      // the fused pass for every clean stretch longer than that
+      g->sp_skip = fails >= 3 ? FU_BACKOFF_MAX : (1u << fails);
       if (fo_only) {
         g->fu_fail_epoch = epoch;
         atomicOr(&g->window_error, 8u);
@@ -377,11 +436,12 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
     }
     if (!fs.applied[k] || i >= E) return;
     FuEv fe;
-    // (no claims: the undo needs the codes, amounts and accounts only)
-    fu_decide(d, i, i > 0 ? U(ev[i - 1].id) : (u128)0, ev[i], g->x_id_max, g->x_sorted, &fe);
+    // (no claims: the undo needs the codes, amounts, fields and accounts only)
+    fu_decide(d, i, i > 0 ? U(ev[i - 1].id) : (u128)0, ev[i], win_ts(w, win_batch(w, i), i), g->x_id_max,
+              g->x_sorted, &fe);
     if (fe.code == TB_CT_OK) {
-      (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.dr].debits_posted), 0ull - fe.amount);
-      (void)atomicAdd(reinterpret_cast<unsigned long long*>(&d.acc[fe.cr].credits_posted), 0ull - fe.amount);
+      (void)atomicAdd(fu_dr_field(d, fe), 0ull - fe.amount);
+      (void)atomicAdd(fu_cr_field(d, fe), 0ull - fe.amount);
     }
     return;
   }
@@ -390,8 +450,9 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
   const bool prefix_win = g->fu_prefix != 0 && mono;
   const unsigned long long bw = g->fu_bad;
   const uint32_t total_bad = (uint32_t)(bw >> 32) == epoch ? (uint32_t)bw : 0u;
-  if (!total_bad && prefix_win && k != gridDim.x - 1) {
-    // nothing moves, nothing to index: only a block where a batch starts has a reply base to write
+  if (!total_bad && prefix_win && k != gridDim.x - 1 && fs.pnmin[k] == ~0ull) {
+    // nothing moves, nothing to index, no expiry entry: only a block where a batch starts has a reply
+    // base to write
     const uint32_t lo = k * FU_T, hi = min(E, lo + FU_T), b = win_batch(w, lo);
     if (w.off[b] != lo && !(b + 1 < w.nb && w.off[b + 1] < hi)) return;
   }
@@ -403,6 +464,8 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
     ex_bad = block_sum<FU_T / 64>(v, lds);
   }
   const bool ok = i < E && ((fs.ok[i >> 6] >> lane) & 1ull);
+  const bool pend = i < E && ((fs.pend[i >> 6] >> lane) & 1ull);
+  const bool pto = i < E && ((fs.pto[i >> 6] >> lane) & 1ull);
   const bool bad = i < E && !ok;
   uint32_t tot;
   const uint32_t rbad = ex_bad + (total_bad ? block_excl<FU_T / 64>(bad ? 1u : 0u, lds, &tot) : 0u);
@@ -430,33 +493,61 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
     for (int q = 0; q < 8; q++) rec[q] = ok ? src[q] : make_uint4(0, 0, 0, 0);
     if (ok) {
       rw_stamp(rec, win_ts(w, win_batch(w, i), i));
-      d.xstatus[base + rins] = 0;
+      d.xstatus[base + rins] = pend ? (uint8_t)TB_PENDING_PENDING : (uint8_t)0;
     }
     const unsigned long long okm = __ballot(ok);
     const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, (int)__builtin_ctzll(okm));
     fu_store_records(d, rec, ok, okm, base + r0, stage + wave * 256);
   }
   if (ok && !prefix_win) x_insert(d.x_tab, d.x_mask, ev[i].id, (uint32_t)(base + rins));
+  {
+    // live expires_at entries of the window's pending creates with a timeout (one atomic per wave)
+    const unsigned long long m = __ballot(pto);
+    if (m) {
+      const int leader = __builtin_ctzll(m);
+      unsigned long long q = 0;
+      if ((int)lane == leader)
+        q = atomicAdd(reinterpret_cast<unsigned long long*>(&g->exp_count), (unsigned long long)__popcll(m));
+      q = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(q >> 32), leader) << 32) |
+          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q, leader);
+      if (pto) {
+        ExpEntry x;
+        x.expires_at = win_ts(w, win_batch(w, i), i) + (uint64_t)ev[i].timeout * TB_NS_PER_S;
+        x.slot = (uint32_t)(base + rins);
+        x.pad = 0;
+        d.exp[*d.exp_cur][q + (unsigned long long)__popcll(m & ((1ull << lane) - 1))] = x;
+      }
+    }
+  }
   if (k == gridDim.x - 1) {
     // the window's totals: the per-block sums folded, the store counts and the window state
-    unsigned long long sum = 0;
+    unsigned long long sum = 0, pn = ~0ull;
     u128 mx = 0;
     for (uint32_t j = threadIdx.x; j < gridDim.x; j += FU_T) {
       sum += fs.pay[j];
       mx = umax128(mx, fs.idmax[j]);
+      pn = fs.pnmin[j] < pn ? fs.pnmin[j] : pn;
     }
     sum = wave_sum_u64(sum);
     mx = wave_max_u128(mx);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long y = __shfl_xor(pn, o, 64);
+      pn = y < pn ? y : pn;
+    }
     if (lane == 0) {
       red[wave] = sum;
       redm[wave] = mx;
+      redp[wave] = pn;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
       for (uint32_t q = 1; q < FU_T / 64; q++) {
         sum += red[q];
         mx = umax128(mx, redm[q]);
+        pn = redp[q] < pn ? redp[q] : pn;
       }
+      if (pn < g->pulse_next) g->pulse_next = pn;  // :1576-1581
       const uint32_t total_ins = E - total_bad;
       for (int32_t bb = (int32_t)w.nb; bb >= 0 && w.off[bb] == E; bb--) o.batch_base[bb] = total_bad;
       if (o.out_count) *o.out_count = total_bad;

@@ -34,5 +34,14 @@ struct GwState {
   uint32_t* ranks;
   uint32_t flags_cap;
   LoadBound* lb;
+  // The scratch engine's accounts persist across consecutive general windows (nothing else changes
+  // them meanwhile; the caller restarts the scratch after any other commit): per owned account the
+  // scratch generation that holds it, per scratch account slot this shard's slot of it (NONE32: another
+  // shard's), the generation, and the scratch's account count before this window's gathered ones.
+  uint32_t* acc_sc;
+  uint32_t* sc2my;
+  uint64_t sc2my_cap;
+  uint32_t sc_gen;
+  uint32_t acc_base;
 };
 

@@ -77,6 +77,32 @@ def exchange_gloo(t):
     torch.cuda.current_stream().synchronize()
 
 
+class _timed:
+    """(rehearsal) wall time of a general-window step on this shard, synced, when gw_times is set:
+    slots 0-1 phase 1 (collect, write), 2-3 phase 2, 4 commit (scratch engine + apply)."""
+
+    def __init__(self, shard, slot):
+        self.shard, self.slot = shard, slot
+
+    def __enter__(self):
+        import time
+
+        if getattr(self.shard, "gw_times", None) is not None:
+            import torch
+
+            torch.cuda.synchronize(self.shard.device)
+            self.t0 = time.perf_counter()
+
+    def __exit__(self, *exc):
+        import time
+
+        t = getattr(self.shard, "gw_times", None)
+        if t is not None and not exc[0]:
+            self.shard.stream.synchronize()
+            t[self.slot] = t.get(self.slot, 0.0) + time.perf_counter() - self.t0
+        return False
+
+
 def home_range(n_batches, shard_count, shard_index):
     """Home batches [first, first + count) of `shard_index`: contiguous, as even as possible."""
     lo = n_batches * shard_index // shard_count
@@ -111,8 +137,11 @@ class ShardedStateMachine:
         self._pulse_next = None  # cached pulse_next_timestamp (order-free windows never change it)
         # general windows: due entries each shard can offer (more sends the window batch by batch)
         self.due_cap = max(4 * batch_max, min(events_max, 1 << 16))
-        self.gxw_events = 0
+        self.gw_events = 0
         self.wscratch = None
+        self.gw_times = None  # (rehearsal: tools/rehearse_shards.py) per-step wall times of general windows
+        self.gw_fallbacks = {"due_overflow": 0, "rejected": 0}  # general windows sent batch by batch
+        self.gw_acc_base = None  # accounts the general windows' scratch engine holds (None: starts over)
         torch.cuda.synchronize(device)
 
     @property
@@ -131,6 +160,7 @@ class ShardedStateMachine:
 
     def prepare_window(self, operation, d_events, batch_events, batch_timestamps):
         """Step 1; returns the facts tensor to be summed across the shards."""
+        self.invalidate_scratch()
         nb = len(batch_events)
         ev = (ctypes.c_uint32 * nb)(*batch_events)
         ts = (ctypes.c_uint64 * nb)(*batch_timestamps)
@@ -192,6 +222,7 @@ class ShardedStateMachine:
         shard; each keeps what it owns."""
         self.sm.open(accounts, transfers, pending_status, account_balances)
         self._pulse_next = None
+        self.invalidate_scratch()
 
     def read_request(self, operation, data):
         """Step 1 of a lookup or query: this shard's part of the read buffer (to be summed)."""
@@ -273,104 +304,136 @@ class ShardedStateMachine:
         pulse_general([self], self._sum, timestamp)
 
     # --------------------------------------------------------------------------------------------
-    # General class, a whole window at a time (csrc/shard_gx.inc tbg_shard_gather_window): one read
-    # set for all of the window's batches, every due entry up to its last batch, the scratch engine
-    # commits the window with its inner pulses modelled (xwin.h), one apply.
+    # General class, a whole window at a time (csrc/shard_gw.inc): each shard lists what it owns of
+    # the window's read set (compact: each object once), the lists are concatenated across the shards
+    # by two rounds of (count exchange, record exchange), every shard's scratch engine commits the
+    # window (the pulses inside it modelled, xwin.h), and each shard applies its own part by position.
     # --------------------------------------------------------------------------------------------
-    def _gxw_init(self, n_events):
+    def _gw_init(self, n_events):
         import torch
 
-        G, D = self.shard_count, self.due_cap
-        need_e = max(n_events, 1)
-        if getattr(self, "gxw_events", 0) >= need_e:
+        if getattr(self, "gw_events", 0) >= max(n_events, 1):
             return
-        L = _lib.lib()
         dev = torch.device("cuda", self.device)
-        p2 = ctypes.c_uint64()
-        nbytes = int(L.tbg_shard_gather_window_bytes(need_e, G, D, ctypes.byref(p2)))
-        self.gxw = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
-        na, nx = 4 * need_e + 2 * G * D, 2 * need_e + G * D + G
-        self.gxw_acc = torch.empty(na * 128, dtype=torch.uint8, device=dev)
-        self.gxw_x = torch.empty(nx * 128, dtype=torch.uint8, device=dev)
-        self.gxw_st = torch.empty(nx, dtype=torch.uint8, device=dev)
-        if getattr(self, "wscratch", None) is not None:
-            self.wscratch.close()
-        self.wscratch = StateMachine(device=self.device, batch_max=self.batch_max, accounts_max=na + 64,
-                                     transfers_max=nx + need_e + 64, window_events_max=need_e)
-        self.gxw_res = torch.zeros(need_e * 8, dtype=torch.uint8, device=dev)
-        self.gxw_base = torch.zeros(WINDOW_BATCHES_MAX + 1, dtype=torch.int32, device=dev)
-        self.gxw_events = need_e
+        need_e = max(n_events, 1)
+        self.gw_cnt = torch.zeros(16 * self.shard_count, dtype=torch.uint8, device=dev)
+        self.gw_res = torch.zeros(need_e * 8, dtype=torch.uint8, device=dev)
+        self.gw_base = torch.zeros(WINDOW_BATCHES_MAX + 1, dtype=torch.int32, device=dev)
+        self.gw_events = need_e
         torch.cuda.synchronize(self.device)
 
-    def gather_window(self, operation, d_events, n_events, t_last, phase):
-        """Gather phase 1 or 2 of a general window; returns the region to be summed across the shards
-        (asynchronous on the engine stream)."""
-        self._gxw_init(n_events)
-        L = _lib.lib()
-        _lib.check(L.tbg_shard_gather_window(self.sm.h, int(operation), d_events, n_events, t_last, phase,
-                                             self.gxw.data_ptr(), self.due_cap), "shard_gather_window")
-        # the regions of THIS window's layout (it depends on the window's event count, not on the
-        # buffer's capacity): every byte the phase wrote must be summed
-        p2 = ctypes.c_uint64()
-        nbytes = int(L.tbg_shard_gather_window_bytes(n_events, self.shard_count, self.due_cap, ctypes.byref(p2)))
-        return self.gxw[: p2.value] if phase == 1 else self.gxw[p2.value: nbytes]
+    def _gw_scratch(self, acc_need, x_need, n_events):
+        """The scratch engine (kept across windows) and the exchange buffers, grown when a window needs
+        more: its account store is bound to gw_acc during a commit, gathered transfers go through gw_x."""
+        import torch
 
-    def due_overflow(self):
-        """After phase 1 was summed: whether a shard had more due entries than the window path holds
-        (then the window goes batch by batch)."""
-        from .state_machine import to_host
-
-        self.stream.synchronize()
-        cnt = to_host(self.gxw[: 4 * self.shard_count]).view(np.uint32)
-        return bool((cnt == 0xFFFFFFFF).any())
-
-    def decide_apply_window(self, operation, d_events, batch_events, batch_timestamps, auto_pulse=False):
-        """After both gathers were summed: the window on the scratch engine (batch 0's harness pulse
-        only with auto_pulse; the later batches' pulses modelled inside it), then the owned objects
-        applied here. Returns the per-batch replies, or None if the scratch engine could not model
-        the window (a pulse inside it reaching the expiry cap, or one reading a balance): nothing was
-        applied then, and the caller commits the window batch by batch."""
-        import time
-
-        from ._lib import RejectedWindow
-        from .state_machine import to_host
-
-        L = _lib.lib()
-        E = sum(batch_events)
-        times = getattr(self, "gxw_times", None)  # (rehearsal) wall time of each step, synced
-        t0 = time.perf_counter()
-        na, nx = ctypes.c_uint64(), ctypes.c_uint64()
-        _lib.check(L.tbg_gathered_objects(self.sm.h, self.gxw.data_ptr(), E, self.due_cap, self.gxw_acc.data_ptr(),
-                                          ctypes.byref(na), self.gxw_x.data_ptr(), self.gxw_st.data_ptr(),
-                                          ctypes.byref(nx)), "gathered_objects")
-        t1 = time.perf_counter()
         sc = self.wscratch
-        sc.reset()
-        _lib.check(L.tbg_open_device(sc.h, self.gxw_acc.data_ptr(), na.value, self.gxw_x.data_ptr(),
-                                     self.gxw_st.data_ptr(), nx.value, self.pulse_next()), "open_device")
-        t2 = time.perf_counter()
-        sc.commit_window(operation, d_events, batch_events, batch_timestamps, self.gxw_res.data_ptr(),
-                         self.gxw_base.data_ptr(), auto_pulse, batch_timestamps[0])
-        try:
-            sc.sync()
-        except RejectedWindow:
+        if sc is not None and self.gw_acc_cap >= acc_need and self.gw_x_cap >= x_need and self.gw_sc_events >= n_events:
+            return
+        acc_cap = max(int(acc_need * 1.25) + 1024, getattr(self, "gw_acc_cap", 0))
+        x_cap = max(int(x_need * 1.25) + 1024, getattr(self, "gw_x_cap", 0))
+        ev_cap = max(n_events, getattr(self, "gw_sc_events", 0))
+        if sc is not None:
+            sc.close()
+        self.gw_acc_base = 0  # (a new scratch holds nothing: only sized when the window starts over)
+        self.wscratch = StateMachine(device=self.device, batch_max=self.batch_max, accounts_max=acc_cap,
+                                     transfers_max=x_cap, window_events_max=ev_cap)
+        dev = torch.device("cuda", self.device)
+        self.gw_acc = torch.empty(acc_cap * 128, dtype=torch.uint8, device=dev)
+        self.gw_x = torch.empty(x_cap * 128, dtype=torch.uint8, device=dev)
+        self.gw_xst = torch.empty(x_cap, dtype=torch.uint8, device=dev)
+        self.gw_acc_cap, self.gw_x_cap, self.gw_sc_events = acc_cap, x_cap, ev_cap
+        torch.cuda.synchronize(self.device)
+
+    def invalidate_scratch(self):
+        """Something other than a general window changed this shard's state: the scratch engine starts
+        over at the next general window (every shard makes the same calls, so every one does)."""
+        self.gw_acc_base = None
+
+    def gw_collect(self, operation, d_events, n_events, t_last, phase, restart=False):
+        """Phase 1 or 2 of a general window: this shard's list of what it owns of the read set (phase 1
+        without the accounts the scratch engine holds from the previous general windows, unless it
+        starts over); returns the count buffer to be summed across the shards (asynchronous)."""
+        self._gw_init(n_events)
+        if phase == 1:
+            restart = restart or self.gw_acc_base is None or self.wscratch is None
+            if restart:
+                self.gw_acc_base = 0
+        xg, nx = (self.gw_x.data_ptr(), self._gw_n[1]) if phase == 2 else (None, 0)
+        with _timed(self, 0 if phase == 1 else 2):
+            _lib.check(_lib.lib().tbg_gw_collect(self.sm.h, int(operation), d_events, n_events, t_last, phase,
+                                                 self.due_cap, xg, nx, self.gw_cnt.data_ptr(), int(restart)),
+                       "gw_collect")
+        return self.gw_cnt
+
+    def gw_plan(self, operation, n_events):
+        """After phase 1's counts were summed: "ok", "restart" (the scratch engine would outgrow its
+        capacity with the accounts it holds: collect again from scratch) or "overflow" (a shard had more
+        entries due than the window path holds: the window goes batch by batch). Sizes the scratch engine
+        for the window's read set (phase 2 adds at most two accounts per gathered transfer)."""
+        from .state_machine import to_host
+
+        with _timed(self, 1):
+            c = to_host(self.gw_cnt).view(np.uint32).reshape(self.shard_count, 4)
+        if (c[:, 3] > self.due_cap).any():
+            self.gw_fallbacks["due_overflow"] += 1
+            self.invalidate_scratch()
+            return "overflow"
+        a1, x1 = int(c[:, 0].sum()), int(c[:, 1].sum())
+        xfer = int(operation) == int(Operation.create_transfers)
+        acc_need = self.gw_acc_base + a1 + 2 * x1 + (0 if xfer else n_events)
+        x_need = x1 + (n_events if xfer else 0)
+        if self.gw_acc_base and (acc_need > self.gw_acc_cap or x_need > self.gw_x_cap or n_events > self.gw_sc_events):
+            self.invalidate_scratch()
+            return "restart"
+        self._gw_scratch(acc_need, x_need, n_events)
+        return "ok"
+
+    def gw_write(self, phase):
+        """After the phase's counts were summed: this shard's records at its offset of the exchange
+        regions; returns the regions to be summed across the shards."""
+        L = _lib.lib()
+        na, nx, ovf = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
+        b = self.gw_acc_base  # (the gathered accounts go after the ones the scratch holds)
+        with _timed(self, 1 if phase == 1 else 3):
+            _lib.check(L.tbg_gw_write(self.sm.h, phase, self.gw_cnt.data_ptr(), self.gw_acc.data_ptr() + b * 128,
+                                      self.gw_acc_cap - b, self.gw_x.data_ptr(), self.gw_xst.data_ptr(), self.gw_x_cap,
+                                      ctypes.byref(na), ctypes.byref(nx), ctypes.byref(ovf)), "gw_write")
+        assert not ovf.value  # (gw_plan checked the due counts)
+        if phase == 1:
+            self._gw_n = [na.value, nx.value]
+            return [self.gw_acc[b * 128: (b + na.value) * 128], self.gw_x[: nx.value * 128], self.gw_xst[: nx.value]]
+        a1 = b + self._gw_n[0]
+        return [self.gw_acc[a1 * 128: (a1 + na.value) * 128]]
+
+    def gw_commit(self, operation, d_events, batch_events, batch_timestamps, auto_pulse):
+        """After both phases were summed: the window on the scratch engine, then this shard's part.
+        Returns the per-batch replies, or None when the scratch engine rejected the window (nothing
+        applied: a pulse inside it reaching the expiry cap, or one falling due in a window that reads
+        balances); the caller then commits it batch by batch."""
+        from .state_machine import to_host
+
+        L = _lib.lib()
+        nb = len(batch_events)
+        ev = (ctypes.c_uint32 * nb)(*batch_events)
+        ts = (ctypes.c_uint64 * nb)(*batch_timestamps)
+        rej, held = ctypes.c_int(), ctypes.c_uint64()
+        with _timed(self, 4):
+            _lib.check(L.tbg_gw_commit(self.sm.h, self.wscratch.h, int(operation), d_events, nb, ev, ts,
+                                       self.gw_acc.data_ptr(), self.gw_acc_base, self.gw_x.data_ptr(),
+                                       self.gw_xst.data_ptr(), self.gw_res.data_ptr(), self.gw_base.data_ptr(),
+                                       int(bool(auto_pulse)), batch_timestamps[0]), "gw_commit")
+            _lib.check(L.tbg_gw_result(self.sm.h, self.wscratch.h, ctypes.byref(rej), ctypes.byref(held)),
+                       "gw_result")
+        self._pulse_next = None
+        if rej.value:
+            self.gw_fallbacks["rejected"] += 1
+            self.invalidate_scratch()  # (its first pulse may have run in the scratch: it starts over)
             return None
-        t3 = time.perf_counter()
-        base = to_host(self.gxw_base)
-        res = to_host(self.gxw_res[: int(base[len(batch_events)]) * 8]).tobytes()
-        replies = [res[base[b] * 8: base[b + 1] * 8] for b in range(len(batch_events))]
-        pa, n_a, px, ps, n_x, pn2 = (ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_void_p(),
-                                     ctypes.c_uint64(), ctypes.c_uint64())
-        _lib.check(L.tbg_device_state(sc.h, ctypes.byref(pa), ctypes.byref(n_a), ctypes.byref(px), ctypes.byref(ps),
-                                      ctypes.byref(n_x), ctypes.byref(pn2)), "device_state")
-        ph, phs = ctypes.c_void_p(), ctypes.c_void_p()
-        _lib.check(L.tbg_device_history(sc.h, ctypes.byref(ph), ctypes.byref(phs)), "device_history")
-        _lib.check(L.tbg_shard_apply(self.sm.h, pa, n_a.value, px, ps, n_x.value, ph, phs, pn2.value), "shard_apply")
-        self._pulse_next = pn2.value
-        if times is not None:
-            self.stream.synchronize()
-            times.append((t1 - t0, t2 - t1, t3 - t2, time.perf_counter() - t3, na.value, nx.value))
-        return replies
+        self.gw_acc_base = held.value
+        base = to_host(self.gw_base)
+        res = to_host(self.gw_res[: int(base[nb]) * 8]).tobytes()
+        return [res[base[b] * 8: base[b + 1] * 8] for b in range(nb)]
 
     def commit_general_window(self, operation, d_events, batch_events, batch_timestamps, auto_pulse=True):
         """A window of the general class with this process's exchange; every shard returns the
@@ -425,6 +488,7 @@ class ShardedStateMachine:
         def recs(off, count):
             return g[off: off + count * 128].view(count, 128)
 
+        self.invalidate_scratch()
         pulse = int(operation) == int(Operation.pulse)
         xfer = int(operation) == int(Operation.create_transfers)
         accs = [recs(lay["ra"], 2 * n), recs(lay["rq"], 2 * G * C)]
@@ -528,20 +592,38 @@ def read_general(shards, summed, operation, data):
 
 
 def commit_general_window(shards, summed, operation, d_events, batch_events, batch_timestamps, auto_pulse=True):
-    """A window of the general class on `shards` (all shards in-process, or this process's one): one
-    read set for all its batches (two exchanges), decided by each shard's scratch engine with the
-    pulses inside the window modelled, one apply. With auto_pulse the harness pulse before batch 0
-    runs with it when due; without, the caller ran it. Returns the per-batch replies; falls back to
-    commit_general_batch per batch (with the harness pulse before batches 1..) when a shard has more
-    due entries than the window path gathers or the scratch engine rejects the window (nothing
-    applied then)."""
+    """A window of the general class on `shards` (all shards in-process, or this process's one): the
+    window's read set gathered in two rounds (csrc/shard_gw.inc), decided by each shard's scratch engine
+    with the pulses inside the window modelled, each shard applying its own part. With auto_pulse the
+    harness pulse before batch 0 runs with it when due; without, the caller ran it. Returns the
+    per-batch replies (the same on every shard; in-process they are checked equal); falls back to
+    commit_general_batch per batch when a shard has more due entries than the window path gathers or
+    the scratch engine rejects the window (nothing applied then)."""
     E = sum(batch_events)
     t_last = batch_timestamps[-1]
-    summed([s.gather_window(operation, d_events, E, t_last, 1) for s in shards])
-    if not any(s.due_overflow() for s in shards[:1]):
-        summed([s.gather_window(operation, d_events, E, t_last, 2) for s in shards])
-        out = [s.decide_apply_window(operation, d_events, batch_events, batch_timestamps, auto_pulse) for s in shards]
+    plan = "ok" if E > 0 else "empty"
+    for attempt in range(2):
+        if plan != "ok":
+            break
+        summed([s.gw_collect(operation, d_events, E, t_last, 1, restart=attempt > 0) for s in shards])
+        plans = [s.gw_plan(operation, E) for s in shards]
+        assert all(p == plans[0] for p in plans)
+        plan = plans[0]
+        if plan == "restart":  # the held accounts and the window's read set exceed the scratch
+            plan = "ok"
+            continue
+        break
+    if plan == "ok":
+        parts = [s.gw_write(1) for s in shards]
+        for k in range(3):
+            summed([p[k] for p in parts])
+        if shards[0]._gw_n[1]:  # (phase 2: the accounts of the gathered transfers)
+            summed([s.gw_collect(operation, d_events, E, t_last, 2) for s in shards])
+            summed([s.gw_write(2)[0] for s in shards])
+        out = [s.gw_commit(operation, d_events, batch_events, batch_timestamps, auto_pulse) for s in shards]
+        assert all((o is None) == (out[0] is None) for o in out)
         if out[0] is not None:
+            assert all(o == out[0] for o in out), "shards decided the window differently"
             return out[0]
     replies, off = [], 0
     for k, (n, T) in enumerate(zip(batch_events, batch_timestamps)):
@@ -562,4 +644,5 @@ def commit_general_batch(shards, summed, operation, d_events, n, timestamp, auto
     summed([s.gather(operation, d_events, n, timestamp, 1) for s in shards])
     summed([s.gather(operation, d_events, n, timestamp, 2) for s in shards])
     replies = [s.decide_apply(operation, d_events, n, timestamp, auto_pulse) for s in shards]
+    assert all(r == replies[0] for r in replies), "shards decided the batch differently"
     return replies[0]

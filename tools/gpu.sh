@@ -8,6 +8,7 @@
 #                                          PMC pass per counter (FETCH_SIZE, WRITE_SIZE), summarised by
 #                                          tools/pmc_summary.py into pmc_NAME.json
 #   tools/gpu.sh rehearse NAME [args]      tools/rehearse_shards.py -> rehearse_NAME.json
+#   tools/gpu.sh py NAME script [args]     any probe script (tools/*.py) -> NAME.json
 # Several commands chain with "+": tools/gpu.sh test + bench default + prof cfg2 --config cfg2
 set -o pipefail
 export TMPDIR=/tmp
@@ -47,6 +48,10 @@ step() {
       local name=$1; shift
       timeout -k 10 600 python -u tools/rehearse_shards.py "$@" > $out/rehearse_$name.json 2> $out/rehearse_$name.err || { echo "rehearse $name failed"; tail -5 $out/rehearse_$name.err; return 1; }
       tail -c 1500 $out/rehearse_$name.json ;;
+    py)
+      local name=$1; shift
+      timeout -k 10 600 python -u "$@" > $out/$name.json 2> $out/$name.err || { echo "$name failed"; tail -5 $out/$name.err; return 1; }
+      tail -c 1500 $out/$name.json ;;
     *) echo "unknown step $cmd"; return 1 ;;
   esac
 }

@@ -26,17 +26,18 @@ BATCH = 8190
 
 
 def general(a):
-    """--stream cfg3|cfg4: the general class (csrc/shard_gx.inc, a whole window per read set) at G
+    """--stream cfg3|cfg4: the general class (csrc/shard_gw.inc, a whole window per read set) at G
     shards on this GPU against ONE unsharded engine on the same stream. Per window and shard, wall
-    time of its steps (gather 1, gather 2, dedupe + scratch open + scratch commit + apply), each
-    shard alone (the in-process sums of the exchanges between them are not counted); the unsharded
-    engine's wall time per window (commit_window + sync) beside it."""
+    time of its steps (gather 1: collect + write, gather 2: collect + write, commit: the scratch
+    engine's window + this shard's apply), each synchronized on its own (the in-process sums of the
+    exchanges between them are not counted); the unsharded engine's wall time per window
+    (commit_window + sync) beside it."""
     import time
 
     import torch
 
     from tigerbeetle_amd import StateMachine, _lib, workload
-    from tigerbeetle_amd.sharding import ShardedStateMachine, pulse_general
+    from tigerbeetle_amd.sharding import ShardedStateMachine, commit_general_window, pulse_general
     from tigerbeetle_amd.state_machine import to_host
     from tigerbeetle_amd.types import NS_PER_S, Operation
 
@@ -47,8 +48,6 @@ def general(a):
     shards = [ShardedStateMachine(G, r, None, batch_max=BATCH, accounts_max=int((n_acc + treasury) / G * 1.2) + 65536,
                                   transfers_max=int((n_x + n_acc) / G * 1.2) + win * BATCH, window_events_max=win * BATCH)
               for r in range(G)]
-    for s_ in shards:
-        s_.gxw_times = []
     one = StateMachine(batch_max=BATCH, accounts_max=n_acc + treasury, transfers_max=n_x + n_acc + win * BATCH,
                        window_events_max=win * BATCH)
     d_acc = torch.empty((n_acc + treasury) * 128, dtype=torch.uint8, device="cuda")
@@ -98,32 +97,20 @@ def general(a):
             one.sync()
             t_one = time.perf_counter() - t0
             want = to_host(d_base)
-            # the shards: batch 0's harness pulse (per-batch general path), then the window
+            # the shards: batch 0's harness pulse (per-batch general path), then the window through
+            # sharding.commit_general_window with each shard's steps timed (csrc/shard_gw.inc)
             if shards[0].pulse(ts[0]):
                 pulse_general(shards, summed, ts[0])
-            per = [[0.0, 0.0, 0.0] for _ in range(G)]
-            E, T = sum(ns), ts[-1]
-            for phase in (1, 2):
-                parts = []
-                for r, s_ in enumerate(shards):
-                    torch.cuda.synchronize()
-                    t0 = time.perf_counter()
-                    parts.append(s_.gather_window(op, ptr, E, T, phase))
-                    s_.stream.synchronize()
-                    per[r][phase - 1] = time.perf_counter() - t0
-                summed(parts)
-                if phase == 1:
-                    assert not shards[0].due_overflow()
-            reps = []
-            for r, s_ in enumerate(shards):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                reps.append(s_.decide_apply_window(op, ptr, ns, ts, False))
-                torch.cuda.synchronize()
-                per[r][2] = time.perf_counter() - t0
-            assert reps[0] is not None, "scratch engine rejected the window"
-            fails = sum(len(x) // 8 for x in reps[0])
+            for s_ in shards:
+                s_.gw_times = {}
+            reps = commit_general_window(shards, summed, op, ptr, ns, ts, auto_pulse=False)
+            per = [[s_.gw_times.get(0, 0.0) + s_.gw_times.get(1, 0.0), s_.gw_times.get(2, 0.0) + s_.gw_times.get(3, 0.0),
+                    s_.gw_times.get(4, 0.0)] for s_ in shards]
+            for s_ in shards:
+                s_.gw_times = None
+            fails = sum(len(x) // 8 for x in reps)
             assert fails == int(want[len(ns)]), (fails, int(want[len(ns)]))
+            E = sum(ns)
             if timed:
                 rows.append((E, t_one, per))
 
@@ -144,14 +131,11 @@ def general(a):
                                    "decide_apply_mean": round(float(steps[:, :, 2].mean()) * 1000, 3),
                                    "max_shard_mean": round(crit / len(timed) * 1000, 3)},
            "estimated_rate_excl_collective": round(ev / crit, 1),
-           "note": "wall clock per step (host launches and syncs included); exchanges summed in-process, not counted"}
-    tt = np.array([t for s_ in shards for t in s_.gxw_times[-len(timed):]])
-    out["decide_apply_split_ms"] = {"objects": round(float(tt[:, 0].mean()) * 1000, 3),
-                                    "reset_open": round(float(tt[:, 1].mean()) * 1000, 3),
-                                    "scratch_commit": round(float(tt[:, 2].mean()) * 1000, 3),
-                                    "apply": round(float(tt[:, 3].mean()) * 1000, 3),
-                                    "objects_accounts_mean": int(tt[:, 4].mean()),
-                                    "objects_transfers_mean": int(tt[:, 5].mean())}
+           "note": "wall clock per step (host launches and syncs included); exchanges summed in-process, not counted",
+           "shard_ms_per_window_split": {"gather1": round(float(steps[:, :, 0].mean()) * 1000, 3),
+                                         "gather2": round(float(steps[:, :, 1].mean()) * 1000, 3),
+                                         "scratch_commit_and_apply": round(float(steps[:, :, 2].mean()) * 1000, 3)}}
+    out["scratch_objects_last_window"] = {"accounts": int(shards[0]._gw_n[0]), "transfers": int(shards[0]._gw_n[1])}
     print(json.dumps(out), flush=True)
     for s_ in shards:
         s_.close()
