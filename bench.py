@@ -11,8 +11,8 @@ src/tigerbeetle/benchmark_load.zig:206-327). `--config` selects the other BASELI
         128-batch windows whose inner pulses the engine models (csrc/xwin.h)
   cfg5  hash-sharded over the N GPUs (default when N > 1): 12.5M accounts and 125M uniform transfers
         per GPU (100M / 1B at N = 8), ~(N-1)/N of the transfers cross-shard; one stream for the whole
-        job, resident in every GPU's HBM; per window two RCCL all-reduces: the per-event owner facts
-        (9 B) and the home shards' commit bits (1 bit) (tigerbeetle_amd/sharding.py, csrc/shard.h)
+        job, resident in every GPU's HBM; per window one RCCL all-reduce of the per-event owner facts
+        (2 B), after which every shard decides every event (tigerbeetle_amd/sharding.py, csrc/shard.h)
 
 A "step" is one create_transfers batch of the stream, committed through the engine's
 device-resident C ABI in windows of --window consecutive batches (tbg_commit_window: pulse
@@ -86,6 +86,7 @@ CONFIGS = {
     # per GPU (weak scaling): 100M accounts / 1B transfers at 8 GPUs
     "cfg5": dict(accounts=12_500_000, transfers=125_000_000, window=64, seed=47, tick=0),
 }
+PENDING_TIMEOUT = 3600  # --pending-every: pending creates that stay pending for the whole run
 CFG3_TREASURY, CFG3_TOP, CFG3_FUND, CFG3_FUND_ID = 1000, 1000, 1_000_000, 10**15
 
 
@@ -159,6 +160,9 @@ def parse():
                    help="cfg1/cfg2: after the timed run, commit this many further batches one at a time through the "
                         "synchronous tbg_prefetch + tbg_commit from host memory (a replica that does not pipeline) and "
                         "report it as `sync_commit` (never `value`); default 64, 0 = off")
+    p.add_argument("--pending-every", type=int, default=0,
+                   help="cfg1/cfg2 mixed stream: every N-th transfer is a pending create (flags.pending, timeout "
+                        "%d s; N=100 is ~1%% pending), 0 = none (the headline stream)" % PENDING_TIMEOUT)
     p.add_argument("--change-log", action="store_true",
                    help="engine keeps the write-back change log (TBG_FLAG_CHANGE_LOG): its device cost")
     a = p.parse_args()
@@ -176,6 +180,8 @@ def parse():
     if a.sync_commit_batches is None:
         a.sync_commit_batches = 64 if a.config in ("cfg1", "cfg2") else 0
     a.tick = c["tick"]
+    if a.pending_every and a.config not in ("cfg1", "cfg2"):
+        p.error("--pending-every applies to the uniform streams (cfg1, cfg2)")
     from tigerbeetle_amd import workload
 
     a.id_order_code = workload.ID_ORDERS[a.id_order]
@@ -213,7 +219,8 @@ class HostStream:
             return self._ids(self.w.transfers_zipf(first, count, self.seed, a.accounts, self.cdf))
         if a.config == "cfg4":
             return self._ids(self.w.transfers_cfg4(first, count, self.seed, a.accounts, BATCH))
-        return self._ids(self.w.transfers_uniform(first, count, self.seed, a.accounts))
+        return self._ids(self.w.mark_pending(self.w.transfers_uniform(first, count, self.seed, a.accounts), first,
+                                             a.pending_every, PENDING_TIMEOUT))
 
 
 def host_cpu():
@@ -247,6 +254,8 @@ def host_fed(args, sm, torch, first, n_acc, seed, win):
     d_tmp = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     _lib.check(L.tbg_gen_transfers_uniform(d_tmp.data_ptr(), first, n, seed, n_acc, 0, sm.stream), "gen")
+    _lib.check(L.tbg_gen_mark_pending(d_tmp.data_ptr(), first, n, args.pending_every, PENDING_TIMEOUT, sm.stream),
+               "pending")
     _lib.check(L.tbg_gen_permute_ids(d_tmp.data_ptr(), n, 1, args.id_order_code, args.perm_seed, sm.stream), "ids")
     sm.sync()
     h_ev = torch.empty(n * 128, dtype=torch.uint8, pin_memory=True)
@@ -286,7 +295,7 @@ def host_fed(args, sm, torch, first, n_acc, seed, win):
 def sync_commit(args, sm, first, n_acc, seed):
     """The replica that does not pipeline: `k` further batches of the same stream, each through the
     synchronous StateMachine calls of the reference protocol (state_machine.zig:2719-2739: pulse()
-    check, prefetch, commit), request bytes in pageable host memory, replies copied back per batch
+    check, prefetch, commit), request bytes in a pinned message pool, replies copied back per batch
     (include/tbg.h tbg_prefetch / tbg_commit). Timed from the first call to the last reply."""
     from tigerbeetle_amd import workload
     from tigerbeetle_amd.types import Operation
@@ -294,8 +303,9 @@ def sync_commit(args, sm, first, n_acc, seed):
     from tigerbeetle_amd.state_machine import HostBuffer
 
     k = args.sync_commit_batches
-    evs = workload.permute_ids(workload.transfers_uniform(first, k * BATCH, seed, n_acc), args.id_order_code,
-                               args.perm_seed)
+    evs = workload.transfers_uniform(first, k * BATCH, seed, n_acc)
+    evs = workload.permute_ids(workload.mark_pending(evs, first, args.pending_every, PENDING_TIMEOUT),
+                               args.id_order_code, args.perm_seed)
     # the replica's message pool: every prepare body lands in a buffer allocated once, pinned
     # (tbg_host_alloc), so the request reaches the device by one DMA
     pool = HostBuffer(k * BATCH * 128)
@@ -393,20 +403,18 @@ def _cpu_baseline(args, seed):
 
 
 # Algorithmic bytes per event of the sharded kernels on one of G shards: every shard
-# reads each event and writes its exchange word and scratch; owned probes / effects are 1/G each.
+# reads each event's ids and writes its facts; owned probes / effects are 1/G each.
 def shard_kernel_bytes(kernel, G, prefix):
     """Algorithmic bytes per window event of the sharded scan / apply kernels (csrc/shard.h)."""
     if kernel == "prep":
-        # k_sh_owned_ct, per window event: the events with an owned role (1 - (1 - 1/G)^3 of them)
-        # are read whole (128) with their list entry (4 read + 4 written) and facts (9) and slots
-        # (8); owned probes: 2 account-table entries 2 x 32, key-map claim 16 (fresh monotonic ids
-        # skip the transfer-id probe)
-        p_own = 1.0 - (1.0 - 1.0 / G) ** 3
-        return p_own * (128 + 8 + 9 + 8) + (2 * 32 + 16) / G
-    # k_sh_apply: roles byte + commit bit; owned: per balance side amount 16 + slot 4 + balance
-    # read+write 64, record read + append 2 x 128, id-table entry 32 unless the window extends the
-    # sorted prefix
-    return 1.125 + (2 * (16 + 4 + 64) + 256 + (0 if prefix else 32)) / G
+        # k_sh_scan, per window event: the ids (64) read by every shard, the 2 B of facts and the roles
+        # byte written; the id owner (1/G) reads the rest of the event (64) and, with monotonic fresh ids,
+        # probes nothing; the account owners (2/G) probe one 32 B table entry and store a 4 B slot
+        return 64 + 3 + 64 / G + 2 * (32 + 4) / G
+    # k_sh_apply: the commit flag and roles byte of every event; owned: per balance side slot 4 +
+    # amount 16 + balance read+write 2 x 16 (no-return 64-bit add), the id owner's record read + append
+    # 2 x 128 and id-table entry 32 unless the window extends the sorted prefix
+    return 2 + (2 * (4 + 16 + 32) + 256 + (0 if prefix else 32)) / G
 
 
 def run_sharded(args, torch, dist, world, rank, device):
@@ -533,7 +541,7 @@ def run_sharded(args, torch, dist, world, rank, device):
             prefix = st["sorted_transfers"] == st["transfers"]
             bytes_launch = int(shard_kernel_bytes(dom, G, prefix) * ev_per_launch)
             achieved = bytes_launch / (us * 1e-6) / 1e9
-            kname = {"prep": "k_sh_owned_ct", "final": "k_sh_apply<true>"}[dom]
+            kname = {"prep": "k_sh_scan<true>", "final": "k_sh_apply<true>"}[dom]
             tr = pmc_traffic("cfg5", kname, ev_per_launch) if G == 1 else None
             roof = {"bound": "hbm", "kernel": kname, "events_per_launch": int(ev_per_launch),
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -541,7 +549,7 @@ def run_sharded(args, torch, dist, world, rank, device):
                     "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
                     "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
                     "phase_avg_us_warmup": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
-                    "exchange_bytes_per_window_per_gpu": (16 + 2 * win * BATCH + 8 * G * 4096) + 16 + win * BATCH // 8}
+                    "exchange_bytes_per_window_per_gpu": 16 + 2 * win * BATCH + 8 * G * 4096}
         line = {
             "metric": "committed transfers/sec (create_transfers)",
             "value": round(timed_events / elapsed, 1),
@@ -559,10 +567,10 @@ def run_sharded(args, torch, dist, world, rank, device):
             "config": {"workload": "cfg5: %d accounts hash-sharded over %d GPU(s), %d uniform create_transfers "
                                    "(%.1f %% cross-shard), %d/batch" % (n_acc, G, n_xfer, 100.0 * (G - 1) / G, BATCH),
                        "batch": BATCH, "window_batches": win, "accounts_per_gpu": args.accounts,
-                       "id_order": args.id_order,
+                       "id_order": args.id_order, "pending_every": args.pending_every,
                        "transfers_per_gpu": args.transfers,
-                       "parallelism": "hash-sharded accounts+ids, home batch ranges, two RCCL all-reduces "
-                                      "per window (owner facts, commit bits)" if G > 1 else "single shard"},
+                       "parallelism": "hash-sharded accounts+ids, home batch ranges, one RCCL all-reduce "
+                                      "per window (owner facts)" if G > 1 else "single shard"},
             "results": {"failed_events_timed": int(timed_fails),
                         "ok_events_per_s": round((timed_events - timed_fails) / elapsed, 1),
                         "shard0_accounts": st["accounts"], "shard0_transfers": st["transfers"],
@@ -672,6 +680,8 @@ def main():
             _lib.check(L.tbg_gen_transfers_cfg4(d_xfer.data_ptr(), 0, n_xfer, seed, n_acc, BATCH, 0, stream), "gen")
         else:
             _lib.check(L.tbg_gen_transfers_uniform(d_xfer.data_ptr(), 0, n_xfer, seed, n_acc, 0, stream), "gen")
+            _lib.check(L.tbg_gen_mark_pending(d_xfer.data_ptr(), 0, n_xfer, args.pending_every, PENDING_TIMEOUT,
+                                              stream), "pending")
     # --id-order: one bijection over every generated id (accounts, funding, transfers)
     for d, n, kind in ((d_acc, n_acc_total, 0), (d_setup, n_setup, 1), (d_xfer, n_xfer, 1)):
         _lib.check(L.tbg_gen_permute_ids(d.data_ptr(), n, kind, args.id_order_code, args.perm_seed, stream), "ids")
@@ -804,7 +814,9 @@ def main():
                              "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None})
         desc = {
             "cfg1": "cfg1: %d accounts, %d uniform create_transfers, %d/batch",
-            "cfg2": "cfg2: %d accounts, %d uniform create_transfers (no flags), %d/batch",
+            "cfg2": "cfg2: %d accounts, %d uniform create_transfers (no flags), %d/batch" if not args.pending_every
+            else "cfg2 mixed: %%d accounts, %%d uniform create_transfers, every %d-th pending (timeout %d s), %%d/batch"
+            % (args.pending_every, PENDING_TIMEOUT),
             "cfg3": "cfg3: %d accounts (Zipf 1.2, debits<=credits limits, pre-funded), %d transfers, %d/batch",
             "cfg4": "cfg4: %d accounts, %d two-phase/linked transfers, +1 s per batch, %d/batch",
         }[cfg] % (n_acc, n_xfer, BATCH)
@@ -823,7 +835,7 @@ def main():
             "dtype": "u128",
             "data": "synthetic (device-generated, seed %d)" % args.seed,
             "config": {"workload": desc, "batch": BATCH, "window_batches": win, "accounts_per_gpu": n_acc,
-                       "id_order": args.id_order,
+                       "id_order": args.id_order, "pending_every": args.pending_every,
                        "transfers_per_gpu": n_xfer, "resolver": args.resolver, "change_log": bool(args.change_log),
                        "parallelism": "independent databases, one per rank (not sharded)" if world > 1 else "single GPU"},
             "results": {"failed_events_timed": int(all_fails),

@@ -164,34 +164,28 @@ void *tbg_stream(tbg_engine *engine);
  * the same commit (state_machine.zig:1220-1306) when accounts are partitioned across engines:
  * account a lives on shard tbg_shard_of(a.id), transfer t on shard tbg_shard_of(t.id). Every shard
  * receives the same window (same arguments as tbg_commit_window) and is the home of a contiguous
- * range of its batches (it decides them and writes their replies):
- *   1. tbg_shard_prepare_window: validates and resolves what it owns (accounts, transfer ids) and
- *      writes tbg_shard_exchange_bytes(operation, E, G) bytes of owner facts at d_exchange (16 B
- *      trailer, then 2 B per create_transfers event plus G x 4096 ledger-mismatch slots of 8 B /
- *      1 B per create_accounts event);
+ * range of its batches (it writes their replies):
+ *   1. tbg_shard_prepare_window: one pass over the window; the owners validate and resolve what they
+ *      own (accounts, transfer ids) and write tbg_shard_exchange_bytes(operation, E, G) bytes of owner
+ *      facts at d_exchange (a 16 B trailer of this shard's verdicts, then 2 B per create_transfers
+ *      event plus G x 4096 ledger-mismatch slots of 8 B / 1 B per create_accounts event);
  *   2. the caller sums those bytes element-wise across all G shards in place, ordered on the engine
  *      stream (ncclAllReduce(uint8, ncclSum) over xGMI, e.g. torch.distributed.all_reduce); every bit
  *      has exactly one writer, so the byte-wise sum is exact;
- *   3. tbg_shard_decide_window: decides the home batches [home_first, home_first + home_count) from
- *      the summed facts; writes their replies (d_results / d_batch_base as tbg_commit_window, for the
- *      home batches only, d_batch_base[0..home_count]) and one commit bit per window event at
- *      d_commit_bits (tbg_shard_commit_bits_bytes(E) bytes: a 16 B trailer of this shard's verdicts
- *      as a home and as an owner, whose sum over the shards is nonzero when the window leaves the
- *      class, then E bits, zero outside the home batches);
- *   4. the caller sums the commit-bit bytes across the shards in place, as in 2;
- *   5. tbg_shard_commit_window: applies only the owned effects of the committed events (the verdict
- *      is the summed trailer of step 4; d_exchange is no longer read, kept for the ABI).
+ *   3. tbg_shard_commit_window: every shard decides every event from the summed facts (the same
+ *      outcome everywhere, so no second exchange), writes the replies of its home batches
+ *      [home_first, home_first + home_count) (d_results / d_batch_base as tbg_commit_window, for the
+ *      home batches only, d_batch_base[0..home_count]) and applies the owned effects of the committed
+ *      events.
  * Sharded class: create_accounts and create_transfers without limits, balancing, two-phase or
  * in-window duplicate ids, overflow-free. Any other window is rejected whole on every shard:
  * tbg_sync returns TBG_E_UNSUPPORTED and no shard has applied it. Asynchronous on the engine stream. */
 uint32_t tbg_shard_of(uint64_t id_lo, uint64_t id_hi, uint32_t shard_count);
 uint64_t tbg_shard_exchange_bytes(uint32_t operation, uint32_t n_events, uint32_t shard_count);
-uint64_t tbg_shard_commit_bits_bytes(uint32_t n_events);
 int tbg_shard_prepare_window(tbg_engine *engine, uint32_t operation, const void *d_events, uint32_t n_batches,
                              const uint32_t *batch_events, const uint64_t *batch_timestamps, void *d_exchange);
-int tbg_shard_decide_window(tbg_engine *engine, const void *d_exchange, uint32_t home_first, uint32_t home_count,
-                            void *d_results, uint32_t *d_batch_base, void *d_commit_bits);
-int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, const void *d_commit_bits);
+int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, uint32_t home_first, uint32_t home_count,
+                            void *d_results, uint32_t *d_batch_base);
 
 /* StateMachine.open (state_machine.zig:527-541), after a restart or a state sync: an empty engine
  * takes the LSM forest's objects: every Account and every Transfer in timestamp order (the grooves'
@@ -433,6 +427,10 @@ int tbg_gen_accounts(void *d_out, uint64_t first, uint64_t count, uint64_t seed,
                      uint16_t flags, void *stream);
 int tbg_gen_transfers_uniform(void *d_out, uint64_t first, uint64_t count, uint64_t seed, uint64_t n_accounts,
                               uint64_t id_offset, void *stream);
+/* Mixed streams: transfer `first + k` of `count` generated records with (first + k) % every == every - 1
+ * becomes a pending create (flags.pending, `timeout` seconds); every == 0 leaves them all. */
+int tbg_gen_mark_pending(void *d_records, uint64_t first, uint64_t count, uint64_t every, uint32_t timeout,
+                         void *stream);
 
 /* Per-phase kernel timing with HIP events on the engine stream. Phases: 0 prep, 1 resolve
  * (account-parallel resolver), 2 classify, 3 wcount, 4 wlist, 5 walk, 6 final, 7 pulse (all five

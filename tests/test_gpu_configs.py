@@ -38,6 +38,14 @@ def test_device_generators_match_numpy():
     assert g.tobytes() == workload.accounts(first, count, 42).tobytes()
     g = _device_gen(L.tbg_gen_transfers_uniform, count, TRANSFER_DTYPE, first, count, 42, 10_000, 7)
     assert g.tobytes() == workload.transfers_uniform(first, count, 42, 10_000, 7).tobytes()
+    d = torch.empty(count * 128, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    _lib.check(L.tbg_gen_transfers_uniform(d.data_ptr(), first, count, 42, 10_000, 7, None), "gen")
+    _lib.check(L.tbg_gen_mark_pending(d.data_ptr(), first, count, 100, 3600, None), "pending")
+    torch.cuda.synchronize()
+    want = workload.mark_pending(workload.transfers_uniform(first, count, 42, 10_000, 7), first, 100, 3600)
+    assert to_host(d).tobytes() == want.tobytes()
+    assert (want["flags"] == 2).sum() == count // 100
     g = _device_gen(L.tbg_gen_accounts_cfg3, count, ACCOUNT_DTYPE, first, count, 43, 130_000, 1000)
     assert g.tobytes() == workload.accounts_cfg3(first, count, 43, 130_000, 1000).tobytes()
     g = _device_gen(L.tbg_gen_funding_cfg3, count, TRANSFER_DTYPE, first, count, 43, 200_000, 100, 10**6, 5)

@@ -139,8 +139,8 @@ class LocalShards:
         return out, False
 
     def commit_window(self, op, batches, tick_ns=0, _pulsed=False):
-        """The harness pulse before the first batch when due, then the five steps of csrc/shard.h
-        with both exchanges summed in-process; returns the per-batch replies assembled from every
+        """The harness pulse before the first batch when due, then the three steps of csrc/shard.h
+        with the exchange summed in-process; returns the per-batch replies assembled from every
         shard's home batches."""
         import torch
 
@@ -160,17 +160,14 @@ class LocalShards:
 
         summed = self.summed
         summed([s.prepare_window(op, d_ev.data_ptr(), ns, ts) for s in self.shards])
-        outs, bits = [], []
+        outs = []
         for s in self.shards:
             first, count = s.home_range(len(ns))
             d_res = torch.zeros(max(sum(ns), 1) * 8, dtype=torch.uint8).cuda()
             d_base = torch.zeros(count + 1, dtype=torch.int32).cuda()
             torch.cuda.synchronize()
-            bits.append(s.decide_window(first, count, d_res.data_ptr(), d_base.data_ptr()))
+            s.commit_prepared(first, count, d_res.data_ptr(), d_base.data_ptr())
             outs.append((first, count, d_res, d_base))
-        summed(bits)
-        for s in self.shards:
-            s.commit_decided()
         for s in self.shards:
             s.sync()
         self._drain()

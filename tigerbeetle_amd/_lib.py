@@ -13,11 +13,11 @@ EXPORTS = [
     "tbg_create", "tbg_destroy", "tbg_input_valid", "tbg_pulse_needed", "tbg_prefetch", "tbg_commit",
     "tbg_commit_device", "tbg_commit_window", "tbg_sync", "tbg_stream", "tbg_setup_balances", "tbg_get_stats",
     "tbg_dump_accounts", "tbg_dump_transfers", "tbg_dump_transfer_status", "tbg_device_stores",
-    "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_gen_permute_ids", "tbg_version", "tbg_debug_last_batch",
+    "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_gen_permute_ids", "tbg_gen_mark_pending", "tbg_version", "tbg_debug_last_batch",
     "tbg_timing_enable", "tbg_timing_collect", "tbg_gen_accounts_cfg3", "tbg_gen_funding_cfg3",
     "tbg_gen_transfers_zipf", "tbg_gen_transfers_cfg4", "tbg_debug_counters", "tbg_shard_of",
-    "tbg_shard_prepare_window", "tbg_shard_decide_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
-    "tbg_shard_commit_bits_bytes", "tbg_window_changes", "tbg_windows_committed",
+    "tbg_shard_prepare_window", "tbg_shard_commit_window", "tbg_shard_exchange_bytes",
+    "tbg_window_changes", "tbg_windows_committed",
     "tbg_open", "tbg_reset", "tbg_prefetch_poll", "tbg_compact", "tbg_checkpoint", "tbg_digest",
     "tbg_commit_window_host", "tbg_host_window_done", "tbg_host_alloc", "tbg_host_free", "tbg_host_register",
     "tbg_host_unregister", "tbg_checksum",
@@ -116,6 +116,7 @@ def lib():
         "tbg_gen_accounts": ([vp, u64, u64, u64, u32, ctypes.c_uint16, ctypes.c_uint16, vp], i32),
         "tbg_gen_transfers_uniform": ([vp, u64, u64, u64, u64, u64, vp], i32),
         "tbg_gen_permute_ids": ([vp, u64, u32, u32, u64, vp], i32),
+        "tbg_gen_mark_pending": ([vp, u64, u64, u64, u32, vp], i32),
         "tbg_version": ([], ctypes.c_char_p),
         "tbg_debug_last_batch": ([vp, vp, vp, u32], i32),
         "tbg_timing_enable": ([vp, ctypes.c_int], i32),
@@ -127,9 +128,7 @@ def lib():
         "tbg_debug_counters": ([vp, vp, u32], i32),
         "tbg_shard_of": ([u64, u64, u32], u32),
         "tbg_shard_prepare_window": ([vp, u32, vp, u32, vp, vp, vp], i32),
-        "tbg_shard_decide_window": ([vp, vp, u32, u32, vp, vp, vp], i32),
-        "tbg_shard_commit_window": ([vp, vp, vp], i32),
-        "tbg_shard_commit_bits_bytes": ([u32], u64),
+        "tbg_shard_commit_window": ([vp, vp, u32, u32, vp, vp], i32),
         "tbg_window_changes": ([vp, vp, u64, P(u64), vp, u64, P(u64), vp, u64, P(u64)], i32),
         "tbg_shard_exchange_bytes": ([u32, u32, u32], u64),
         "tbg_windows_committed": ([vp, P(u64), P(u64)], i32),

@@ -149,7 +149,7 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t sh_unsup;       // sharded: a home event outside the class this window (k_sh_reply -> trailer 2)
   uint64_t ovf_rescans;    // times ovf_bound was re-tightened to the accounts' largest balance sum (restore.h)
   uint32_t fu_nonmono;     // the epoch of a fused window whose ids did not all rise (claim mode, fused.h)
-  uint32_t pad5;
+  uint32_t sh_done;        // sharded: blocks of k_sh_scan / k_sh_apply finished (the last one folds, shard.h)
 };
 
 // The fused pass (fused.h) committed this window: the general path's kernels return at once.
@@ -285,11 +285,37 @@ __device__ inline uint32_t x_find(const XEntry* __restrict__ tab, const tb_trans
   return x_probe_from(tab, xr, mask, h, tab[h & mask], id);
 }
 
-// Binary search of the sorted transfer prefix [0, P) (Globals::x_sorted), in u128 id order.
+__device__ inline double u128_to_double(u128 v) {
+  return (double)(uint64_t)(v >> 64) * 18446744073709551616.0 + (double)(uint64_t)v;
+}
+
+// Search of the sorted transfer prefix [0, P) (Globals::x_sorted), in u128 id order. The prefix's ids
+// are mostly dense runs (sequential ids; time-based ids spread evenly within a millisecond), so a few
+// interpolation steps narrow the range to the key's neighbourhood (one step for a dense run) before a
+// binary search: a post/void of a prefix transfer no longer pays ~log2(P) dependent loads. Each step
+// keeps the invariant that the key, if present, is in [lo, hi).
 __device__ inline uint32_t x_prefix_find(const tb_transfer_t* __restrict__ xr, uint64_t P, tb_uint128_t id) {
   if (P == 0) return NONE32;
   const u128 key = U(id);
-  uint64_t lo = 0, hi = P;
+  u128 a = U(xr[0].id), b = U(xr[P - 1].id);
+  if (key < a || key > b) return NONE32;
+  if (key == a) return 0;
+  if (key == b) return (uint32_t)(P - 1);
+  uint64_t lo = 1, hi = P - 1;  // a < key < b
+  for (int it = 0; it < 4 && hi - lo > 16; it++) {
+    const double f = u128_to_double(key - a) / u128_to_double(b - a);
+    uint64_t mid = lo + (uint64_t)(f * (double)(hi - lo));
+    if (mid >= hi) mid = hi - 1;
+    const u128 km = U(xr[mid].id);
+    if (km == key) return (uint32_t)mid;
+    if (km < key) {
+      lo = mid + 1;
+      a = km;
+    } else {
+      hi = mid;
+      b = km;
+    }
+  }
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
     if (U(xr[mid].id) < key)

@@ -2,39 +2,30 @@
 //
 // Ownership: an account belongs to shard_of(account id), a transfer to shard_of(transfer id). Every
 // shard holds the whole prepared window in HBM (the replica hands each GPU the same prepare body).
-// Each shard is also the HOME of a contiguous range of the window's batches: it decides those events
-// and writes their replies. Per-shard work is the window's ids (64 B per event) plus 1/G of
-// everything else, so the work per GPU falls as G grows:
+// Each shard is also the HOME of a contiguous range of the window's batches: it writes their replies.
+// Per window, three launches and one exchange:
 //
-//   k_sh_roles    whole window: the ids of each event (64 B); events with a role this shard owns
-//                 (debit account, credit account, transfer id) are compacted, in event order, into
-//                 per-segment lists, so the owned work below runs on dense waves.
-//   k_sh_owned_*  owned events only: the id owner reads the event whole and validates it
-//                 (state_machine.zig:1424-1439, 1465-1489); if it reaches the account checks, it
-//                 claims the id (in-window duplicates through the window key map) and compares it
-//                 with a stored transfer (`exists`, :1506-1507). The debit / credit owners read the
-//                 account ids and the amount and resolve their account (ledger, limit flag). Each
-//                 owner writes its part of the event's 9 B of facts (exchange 1).
+//   k_sh_scan     one pass over the window, one event per thread: the ids (64 B) give the owners; the
+//                 id owner validates the event (state_machine.zig:1424-1439, 1465-1489), claims the id
+//                 when the window's ids are not known to rise, and compares it with a stored transfer
+//                 (`exists`, :1506-1507); the debit / credit owners resolve their account (state
+//                 against the event's ledger, limit flags) and keep its slot. Each owner writes its part
+//                 of the event's 2 B of facts; the last block folds this shard's verdicts.
 //   (caller)      exchange 1: byte-wise sum all-reduce of the facts (RCCL over xGMI). Every bit has
 //                 exactly one writer, so the sum is the union.
-//   k_sh_home_*   home slice: validation codes and class checks.
-//   k_sh_decide   home slice: account lookups (:1496-1497), ledgers (:1503-1504), exists, then linked
-//                 chains (:1240-1300).
-//   k_sh_reply    home slice: per-batch replies (failure ranks from k_sh_decide's per-segment
-//                 counts); one commit bit per event (exchange 2). Block 0 folds the owned work's
-//                 partials into this shard's owner verdicts (k_sh_close does it for a shard home to
-//                 no event).
-//   (caller)      exchange 2: byte-wise sum all-reduce of the commit bits (E/8 B) and the verdicts.
-//   k_sh_icount, k_sh_apply  whole window, owned roles only: the verdict, then the account owners add
-//                 the amounts (exact 128-bit atomics) and the id owner appends the record.
+//   k_sh_decide   every event on every shard, from the facts alone: account lookups (:1496-1497),
+//                 ledgers (:1503-1504), exists, linked chains (:1240-1300). The same outcome on every
+//                 shard, so no second exchange (round 4 decided on the homes and all-reduced commit bits).
+//   k_sh_apply    the home batches' replies; the account owners add the amounts, the id owner appends
+//                 the record.
 //
 // The sharded class is the order-free one: no balance read (no limit flag on a touched
 // account, no balancing), no history row (no flags.history on a touched account), no two-phase, no
-// in-window duplicate id, overflow-free window. Then every
-// event's outcome is a function of the owners' facts alone, and the effects commute. A window outside
-// the class is detected before anything is applied (by an owner or a home: exchange 2's trailer), so
-// every shard reaches the same verdict and the window fails with
-// TBG_E_UNSUPPORTED at tbg_sync: no shard applies any of it.
+// in-window duplicate id, overflow-free window. Then every event's outcome is a function of the owners'
+// facts alone, and the effects commute. A window outside the class is detected before anything is
+// applied (by an owner: exchange 1's trailer; by every shard's decide: a committed event reading a
+// balance), so every shard reaches the same verdict and the window fails with TBG_E_UNSUPPORTED at
+// tbg_sync: no shard applies any of it.
 #pragma once
 #include "changes.h"
 #include "sm_logic.h"
@@ -43,21 +34,18 @@
 
 // Exchange bytes of a window of E events over G shards (summed byte-wise over the shards: every bit
 // has exactly one writer, so the byte sum is the union with no carries; one uint8 all-reduce):
-//   [0, 16)         trailer: unused, zero (the owners' verdicts travel in exchange 2's)
-//   [16, 16+E)      bits 0-5: 1 + (TB_CT_OK or the exists* code; create_accounts: 1 + the code), by
-//                   the id owner; bit 6: the debit account has debits_must_not_exceed_credits or
-//                   flags.history (its owner); bit 7: the credit account has
-//                   credits_must_not_exceed_debits or flags.history (its owner)
+//   [0, 16)         trailer: word 0 this shard's verdict bytes (k_sh_scan; ZW_* below), the rest zero
+//   [16, 16+E)      the id owner's byte: 1 + the code, static / linked bits (ZW_*)
 //   create_transfers:
 //   [16+E, 16+2E)   the account sides' states (SH_ACC_*): bits 0-1 the debit account, 2-3 the credit
-//                   account, each by its owner against the event's ledger
+//                   account, each by its owner against the event's ledger; bits 4 / 5 the limit or
+//                   history flag of the debit / credit account
 //   [16+2E, ...)    G x SH_MIS_SLOTS u64 ledger-mismatch slots, shard g's at [g * SH_MIS_SLOTS, ...):
 //                   valid << 63 | side << 52 | event << 32 | the account's ledger
 // A side's ledger is needed only when both accounts mismatch the event's ledger (then whether they
 // match each other decides between accounts_must_have_the_same_ledger and
 // transfer_must_have_the_same_ledger_as_accounts, :1503-1504), so the 8 B of ledgers per event of the
 // first protocol are 2 bits of state per side plus rare mismatch slots: 2 B per event instead of 9.
-enum : uint32_t { SH_Z_MASK = 0x3F, SH_DR_LIMIT = 0x40, SH_CR_LIMIT = 0x80 };
 enum : uint32_t { SH_ACC_OK = 1, SH_ACC_MISSING = 2, SH_ACC_MISMATCH = 3 };
 #define SH_MIS_SLOTS 4096u  // per shard; more mismatches in one window: outside the class (trailer 0)
 
@@ -158,89 +146,10 @@ __device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bo
   g->batch_huge = 0;
 }
 
-// Exchange 2 (commit bits): 16 B trailer, 4 x u32 summed over the shards: [0] homes that found an
-// event outside the class, [1] shards that saw an in-window duplicate id or overflowed their
-// ledger-mismatch slots, [2] shards over capacity, [3] shards whose overflow bound does not clear
-// the window's amounts; then one bit per event, in 64-bit words (a word may hold bits of two homes: distinct bits).
-__host__ __device__ inline uint64_t xch2_bytes(uint32_t E) { return 16 + 8ull * ((E + 63) / 64); }
-
 // Scan-block partials (Scratch::blk_aux): bit 0 huge amount, bit 1 in-window duplicate id (outside the
 // class), bit 2 ids not strictly increasing (or >= 2^64), bit 3 the window's first id is above every
-// stored id, owned ids reaching the exists check << 4.
-enum : uint32_t { SHX_HUGE = 1, SHX_DUP = 2, SHX_NONMONO = 4, SHX_FRESH = 8, SHX_OWN_SHIFT = 4 };
-
-// After exchange 1 (stream-ordered, one 1024-thread block, red[] one entry per wave: block 0 of
-// k_sh_reply, or k_sh_close when this shard is home to no event): folds the scan blocks' partials
-// (no same-address atomics across blocks) into this shard's window verdicts, returned to thread 0 as bit 0 (duplicate id or
-// mismatch slots overflowed), bit 1 (capacity), bit 2 (overflow bound), and sets
-// Globals::win_flags bit 1 (the owned records extend the sorted prefix) and small_win for k_sh_apply.
-// The verdicts travel in exchange 2's trailer, so exchange 1 needs no fold before it.
-__device__ inline uint32_t sh_close_fold(Dev d, const Scratch& s, uint32_t nblk, uint32_t xfer, u128* red,
-                                         uint32_t* bits_s, unsigned long long* own_s) {
-  if (threadIdx.x == 0) {
-    *bits_s = 0;
-    *own_s = 0;
-  }
-  __syncthreads();
-  u128 v = 0;
-  uint32_t a = 0;
-  unsigned long long own = 0;
-  for (uint32_t j = threadIdx.x; j < nblk; j += 1024) {
-    const uint32_t x = s.blk_aux[j];
-    a |= x & 15u;
-    own += x >> SHX_OWN_SHIFT;
-    if (xfer) v += s.blk_amt[j];
-  }
-  if (a) atomicOr(bits_s, a);
-  if (own) atomicAdd(own_s, own);
-  // the amounts: wave sums of the two 64-bit halves, one LDS word per wave, one barrier
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t lo = __shfl_xor((unsigned long long)(uint64_t)v, o, 64);
-    const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(v >> 64), o, 64);
-    v += ((u128)hi << 64) | lo;
-  }
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();  // (also orders the LDS atomics above before thread 0 reads them)
-  if (threadIdx.x != 0) return 0;
-  u128 tot = 0;
-  for (uint32_t w2 = 0; w2 < blockDim.x / 64; w2++) tot += red[w2];
-  Globals* g = d.g;
-  const uint32_t bits = *bits_s;
-  uint32_t verdict = (bits & SHX_DUP) ? 1u : 0u;
-  if (xfer) {
-    g->batch_amount_sum += tot;
-    if (bits & SHX_HUGE) g->batch_huge = 1;
-    if (g->x_count + *own_s > d.x_max) verdict |= 2u;
-    if (window_ovf_mode(g)) verdict |= 4u;
-    // every owned balance field stays below 2^64 this window: k_sh_apply's adds need no carry
-    const u128 top = g->ovf_bound + g->batch_amount_sum;
-    g->small_win = (!g->batch_huge && top >= g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1u : 0u;
-    const bool prefix = !(bits & SHX_NONMONO) && (bits & SHX_FRESH) && g->x_sorted == g->x_count;
-    g->win_flags = prefix ? 2u : 0u;
-  } else {
-    if (g->acc_count + *own_s > d.acc_max) verdict |= 2u;
-  }
-  return verdict;
-}
-
-// Exchange 2's trailer, written whole by thread 0: the homes' out-of-class flag (k_sh_home /
-// k_sh_decide) and this shard's owner verdicts (sh_close_fold), one word each.
-__device__ inline void sh_trailer2(uint32_t* trailer2, uint32_t unsup, uint32_t verdict) {
-  trailer2[0] = unsup;
-  trailer2[1] = verdict & 1u;
-  trailer2[2] = (verdict >> 1) & 1u;
-  trailer2[3] = (verdict >> 2) & 1u;
-}
-
-// A shard home to no event of the window still folds its owner verdicts into exchange 2.
-__global__ void __launch_bounds__(1024) k_sh_close(Dev d, Scratch s, uint32_t nblk, uint32_t xfer, uint32_t* trailer2) {
-  __shared__ u128 red[1024 / 64];
-  __shared__ uint32_t bits_s;
-  __shared__ unsigned long long own_s;
-  const uint32_t verdict = sh_close_fold(d, s, nblk, xfer, red, &bits_s, &own_s);
-  if (threadIdx.x == 0) sh_trailer2(trailer2, 0u, verdict);
-}
+// stored id, bit 4 an event outside the class (SHX_UNSUP), owned ids reaching the exists check << 5.
+enum : uint32_t { SHX_HUGE = 1, SHX_DUP = 2, SHX_NONMONO = 4, SHX_FRESH = 8, SHX_OWN_SHIFT = 5 };
 
 // Validation a create_transfers event gets on every shard that looks at it whole (its owners and its
 // home): timestamp (:1253-1259), head and field checks (:1465-1489, 1614-1624). Returns the static
@@ -284,67 +193,6 @@ __device__ inline uint32_t sh_static_ca(const tb_account_t& a, uint32_t* cls, bo
   return code;
 }
 
-// Owned roles of an event (Scratch::bstatus): it reaches the account checks and this shard owns its
-// debit account / credit account / id.
-enum : uint8_t { ROLE_DR = 1, ROLE_CR = 2, ROLE_ID = 4 };
-
-// ------------------------------------------------------------------------------------------------
-// scan, in two passes so that the long dependent chains (validation, probes, claims) run on dense
-// waves: k_sh_roles reads the ids of every event and compacts the events with an owned role, in
-// event order, into per-segment lists (Scratch::wlist, segment k at k * SEG, Scratch::cnt_w[k]
-// entries: event | candidate roles << 24); k_sh_owned works through those lists.
-// ------------------------------------------------------------------------------------------------
-__device__ inline uint32_t ol_event(uint32_t x) { return x & 0xFFFFFFu; }
-__device__ inline uint32_t ol_roles(uint32_t x) { return x >> 24; }
-
-template <bool XFER>
-__global__ void __launch_bounds__(SEG) k_sh_roles(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes, uint32_t E,
-                                                  XchView xch, uint32_t G, uint32_t me) {
-  __shared__ uint32_t lds[SEG / 64];
-  __shared__ uint32_t aux;
-  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
-  if (threadIdx.x == 0) aux = 0;
-  // exchange 1's trailer (written by later kernels of the window only): zeroed here, not by a memset;
-  // so is the homes' out-of-class flag that k_sh_reply turns into exchange 2's trailer
-  if (i < 4) xch.trailer[i] = 0;
-  if (i == 0) d.g->sh_unsup = 0;
-  __syncthreads();
-  uint32_t roles = 0;
-  if (i < E) {
-    const uint4* q = reinterpret_cast<const uint4*>(ev_bytes + (size_t)i * 128);
-    const tb_uint128_t id = rw_u128(q[0]);
-    if (shard_of(id.lo, id.hi, G) == me) roles |= ROLE_ID;
-    if (XFER) {
-      const tb_uint128_t dra = rw_u128(q[1]), cra = rw_u128(q[2]);
-      if (shard_of(dra.lo, dra.hi, G) == me) roles |= ROLE_DR;
-      if (shard_of(cra.lo, cra.hi, G) == me) roles |= ROLE_CR;
-      // the owned records extend the sorted prefix if the window's ids are strictly increasing
-      bool nm = false;
-      if (i > 0) nm = !(U(id) > U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i - 1].id));
-      if (nm) atomicOr(&aux, (uint32_t)SHX_NONMONO);
-      if (i == 0 && U(id) > d.g->x_id_max) atomicOr(&aux, (uint32_t)SHX_FRESH);
-      xch.acc[i] = 0;  // k_sh_owned writes the owned facts
-    }
-    xch.zw[i] = 0;
-  }
-  if (XFER) {  // the mismatch slots (every shard's, zero but its own writes) and this shard's count
-    for (uint32_t k = i; k < G * SH_MIS_SLOTS; k += gridDim.x * SEG) xch.mis[k] = 0;
-    if (i == 0) d.g->sh_mis = 0;
-  }
-  uint32_t tot;
-  const uint32_t r = block_excl<SEG / 64>(roles ? 1u : 0u, lds, &tot);
-  if (roles) s.wlist[blockIdx.x * SEG + r] = i | (roles << 24);
-  if (threadIdx.x == 0) {
-    s.cnt_w[blockIdx.x] = tot;
-    s.blk_aux[blockIdx.x] = aux;
-  }
-}
-
-// Owned work of segment blockIdx.x: the owner facts. The id owner reads the event whole, validates
-// it and, if it reaches the account checks, claims the id and compares it with a stored transfer.
-// The account owners need no validation: they read the account ids and the amount only (facts of an
-// event its home rejects statically are never read, and the commit bit gates every effect); every
-// amount they see counts toward the overflow bound, valid or not. Rewrites each entry's roles to the
 // A sharded window runs no pulse: the caller ran the harness pulse before its first batch when one
 // was due (through the general path), so no pulse may be due at any of its batches
 // (pulse_next > T_last), and a window of several batches spans less than a second. The class holds
@@ -356,93 +204,148 @@ __device__ inline void check_window(const WinDesc& w, Globals* g) {
   if (last >= g->pulse_next || (w.nb > 1 && last >= first_ts + TB_NS_PER_S)) atomicOr(&g->window_error, 8u);
 }
 
-// ones that carry effects.
-__global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_transfer_t* __restrict__ ev, WinDesc w,
-                                                     uint32_t epoch, XchView xch, uint32_t me) {
-  __shared__ u128 red[SEG / 64];
+
+// Owned roles of an event (Scratch::bstatus, k_sh_scan): this shard owns its debit account / credit
+// account / id.
+enum : uint8_t { ROLE_DR = 1, ROLE_CR = 2, ROLE_ID = 4 };
+
+// Exchange 1, per event: the id owner's byte (XchView::zw): bits 0-5 1 + the code, bit 6 the code is
+// static (validation, final before the account checks), bit 7 the event is linked (every shard's
+// k_sh_decide follows the chains); the account byte (XchView::acc): bits 0-1 / 2-3 the debit / credit
+// side's state (SH_ACC_*), bit 4 / 5 the debit / credit account has a limit or flags.history (each by
+// its owner). The trailer's first word: one verdict byte per kind, 0 or 1 on each shard (the byte sum
+// over the shards is nonzero iff one shard's is): [0] an in-window duplicate id, ids that did not rise
+// in a window that made no claims, or the ledger-mismatch slots overflowed; [1] capacity; [2] the
+// overflow bound; [3] an event outside the class (pending, balancing, post/void).
+enum : uint32_t { ZW_CODE = 0x3F, ZW_STATIC = 0x40, ZW_LINKED = 0x80, ACC_DR_LIMIT = 0x10, ACC_CR_LIMIT = 0x20 };
+static_assert(TB_CT_EXCEEDS_DEBITS + 1 <= (int)ZW_CODE && TB_CA_EXISTS + 1 <= (int)ZW_CODE, "codes fit 6 bits");
+enum : uint32_t { SHX_UNSUP = 16 };
+#define SH_SCAN_T 256  // k_sh_scan's block: small blocks keep more of its latency-bound waves resident
+
+__device__ inline bool sh_verdict(const XchView& x) { return x.trailer[0] != 0; }
+
+// ------------------------------------------------------------------------------------------------
+// k_sh_scan (before exchange 1): one pass over the window, one event per thread, every shard. Each
+// event's ids give its owners (64 B read); the owners do their part in the same pass: the id owner
+// validates the event (state_machine.zig:1424-1439, 1465-1489), claims its id when the window's ids
+// are not known to rise (in-window duplicates through the window key map) and compares it with a
+// stored transfer (`exists`, :1506-1507); the debit / credit owners resolve their account (state
+// against the event's ledger, limit and history flags) and keep its slot for k_sh_apply. Then
+// k_sh_fold (one block) folds the blocks' partials into this shard's verdicts (exchange 1's trailer)
+// and the window's overflow / prefix state. (A last-block-done fold inside the scan measured ~2x
+// slower: its agent-scope fence per block writes the XCD's L2 back.)
+// ------------------------------------------------------------------------------------------------
+template <bool XFER>
+__global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes,
+                                                       WinDesc w, uint32_t epoch, XchView xch, uint32_t G, uint32_t me) {
+  __shared__ u128 red[SH_SCAN_T / 64];
   __shared__ uint32_t aux;
-  const uint32_t k = blockIdx.x * SEG + threadIdx.x;
-  if (threadIdx.x == 0) aux = 0;
-  if (k == 0) check_window(w, d.g);
-  // Window ids strictly increasing (k_sh_roles' per-segment bits, one launch per segment here too):
-  // no in-window duplicate id can exist, so the id owner skips the key-map claim, a returning CAS per
-  // owned id (the sharded path reads the key map for nothing else). Other blocks may be OR-ing
-  // their own bits into these words meanwhile; bit SHX_NONMONO is never among them.
-  uint32_t nm = 0;
-  for (uint32_t j = threadIdx.x; j < gridDim.x; j += SEG)
-    nm |= __hip_atomic_load(&s.blk_aux[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & (uint32_t)SHX_NONMONO;
-  const bool mono = !__syncthreads_or((int)nm);
-  u128 amount_upper = 0;
-  const uint32_t n = s.cnt_w[blockIdx.x];
-  bool owned_id = false;
-  if (threadIdx.x < n) {
-    const uint32_t x = s.wlist[k];
-    const uint32_t i = ol_event(x), cand = ol_roles(x);
-    uint32_t roles = 0, zw = 0;
-    if (cand & ROLE_ID) {
-      tb_transfer_t t = ev[i];
-      uint32_t cls = 0;
-      bool reach, unsup;
-      (void)sh_static_ct(t, w, win_batch(w, i), i, &cls, &reach, &unsup);
-      if (reach) {
-        roles |= ROLE_ID;
-        owned_id = true;
-        bool dup = false;
-        if (!mono) (void)sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), t.id, i, w.E, epoch, &dup);
-        if (dup) atomicOr(&aux, (uint32_t)SHX_DUP);
-        uint32_t xs = NONE32;
-        if (x_may_exist(t.id, d.g->x_id_max)) {
-          xs = x_find(d.x_tab, d.xr, d.x_mask, t.id);
-          if (xs == NONE32) xs = x_prefix_find(d.xr, d.g->x_sorted, t.id);
-        }
-        zw |= 1 + (xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]));
-      }
+  const uint32_t i = blockIdx.x * SH_SCAN_T + threadIdx.x;
+  const uint32_t E = w.E;
+  Globals* g = d.g;
+  if (threadIdx.x == 0) {
+    aux = 0;
+    if ((i & (SEG - 1)) == 0) {  // this segment's counters (k_sh_decide adds to them)
+      s.cnt_bad[i / SEG] = 0;
+      s.cnt_ins[i / SEG] = 0;
     }
-    if (cand & (ROLE_DR | ROLE_CR)) {
-      const uint4* q = reinterpret_cast<const uint4*>(ev + i);
-      const uint4 q1 = q[1], q2 = q[2], q3 = q[3];
-      const uint32_t ledger = q[7].x;  // the event's ledger: each side's state is against it
-      amount_upper = U(rw_u128(q3));
-      uint32_t acc = 0;
-      // up to two independent probes, one per owned side
+  }
+  if (i == 0) check_window(w, g);
+  if (XFER)  // the other shards' mismatch slots are zero in this shard's copy (its own: k_sh_fold)
+    for (uint32_t k = i; k < G * SH_MIS_SLOTS; k += gridDim.x * SH_SCAN_T)
+      if (k / SH_MIS_SLOTS != me) xch.mis[k] = 0;
+  __syncthreads();
+  // the previous fast-path window's ids did not all rise: claims find in-window duplicates
+  const bool claim = !XFER || g->mono_prev == 0;
+  uint32_t roles = 0, zw = 0, accb = 0;
+  u128 amount = 0;
+  bool owned_id = false;
+  if (i < E) {
+    const uint4* q = reinterpret_cast<const uint4*>(ev_bytes + (size_t)i * 128);
+    const tb_uint128_t id = rw_u128(q[0]);
+    if (shard_of(id.lo, id.hi, G) == me) roles |= ROLE_ID;
+    uint4 q1 = make_uint4(0, 0, 0, 0), q2 = q1;
+    if (XFER) {
+      q1 = q[1];
+      q2 = q[2];
+      const tb_uint128_t dra = rw_u128(q1), cra = rw_u128(q2);
+      if (shard_of(dra.lo, dra.hi, G) == me) roles |= ROLE_DR;
+      if (shard_of(cra.lo, cra.hi, G) == me) roles |= ROLE_CR;
+      // the window's ids strictly increasing (every shard reads every id: the same verdict everywhere)
+      if (i > 0 && !(U(id) > U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i - 1].id)))
+        atomicOr(&aux, (uint32_t)SHX_NONMONO);
+      if (i == 0 && U(id) > g->x_id_max) atomicOr(&aux, (uint32_t)SHX_FRESH);
+    }
+    if (roles & ROLE_ID) {
+      uint32_t cls = 0;
+      bool reach, unsup = false, dup = false;
+      uint32_t code;
+      if (XFER) {
+        tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
+        code = sh_static_ct(t, w, win_batch(w, i), i, &cls, &reach, &unsup);
+        if (reach) {
+          if (claim)
+            (void)sh_claim(g, s.bmap, s.bmask, ev_bytes, t.id, i, E, epoch, &dup);
+          uint32_t xs = NONE32;
+          if (x_may_exist(t.id, g->x_id_max)) {
+            xs = x_find(d.x_tab, d.xr, d.x_mask, t.id);
+            if (xs == NONE32) xs = x_prefix_find(d.xr, g->x_sorted, t.id);
+          }
+          code = xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]);
+        }
+      } else {
+        const tb_account_t a = reinterpret_cast<const tb_account_t*>(ev_bytes)[i];
+        code = sh_static_ca(a, &cls, &reach);
+        if (reach) {
+          (void)sh_claim(g, s.bmap, s.bmask, ev_bytes, a.id, i, E, epoch, &dup);
+          AccEntry ae;
+          const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, a.id, &ae);
+          code = slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(a, d.acc[slot]);
+        }
+      }
+      owned_id = reach;
+      if (dup) atomicOr(&aux, (uint32_t)SHX_DUP);
+      if (unsup) atomicOr(&aux, (uint32_t)SHX_UNSUP);
+      zw = (1u + code) | (reach ? 0u : (uint32_t)ZW_STATIC) | ((cls & C_LINKED) ? (uint32_t)ZW_LINKED : 0u);
+    }
+    if (XFER && (roles & (ROLE_DR | ROLE_CR))) {
+      // every amount an account owner sees counts toward the overflow bound, valid event or not
+      amount = U(rw_u128(q[3]));
+      const uint32_t ledger = q[7].x;  // each side's state is against the event's ledger
 #pragma unroll
       for (uint32_t side = 0; side < 2; side++) {
-        if (!(cand & (side ? ROLE_CR : ROLE_DR))) continue;
-        roles |= side ? ROLE_CR : ROLE_DR;
+        if (!(roles & (side ? ROLE_CR : ROLE_DR))) continue;
         AccEntry e;
         const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, rw_u128(side ? q2 : q1), &e);
         (side ? s.cr_slot : s.dr_slot)[i] = slot;
         uint32_t st = SH_ACC_MISSING;
         if (slot != NONE32) {
           st = e.ledger == ledger ? SH_ACC_OK : SH_ACC_MISMATCH;
-          // a limit (a balance read) or flags.history (a historical_balance row of balances after
-          // the event, :1806-1841): outside the order-free class if the event commits
+          // a limit (a balance read) or flags.history (a historical_balance row of balances after the
+          // event, :1806-1841): outside the order-free class if the event commits
           const uint16_t lim = side ? TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS : TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS;
-          if (e.flags & (lim | TB_ACCOUNT_HISTORY)) zw |= side ? SH_CR_LIMIT : SH_DR_LIMIT;
+          if (e.flags & (lim | TB_ACCOUNT_HISTORY)) accb |= side ? ACC_CR_LIMIT : ACC_DR_LIMIT;
           if (st == SH_ACC_MISMATCH) {
-            const uint32_t k2 = atomicAdd(&d.g->sh_mis, 1u);
+            const uint32_t k2 = atomicAdd(&g->sh_mis, 1u);
             if (k2 < SH_MIS_SLOTS)
               xch.mis[me * SH_MIS_SLOTS + k2] = (1ull << 63) | ((unsigned long long)side << 52) |
                                                 ((unsigned long long)i << 32) | e.ledger;
             else
-              atomicOr(&aux, (uint32_t)SHX_DUP);  // (trailer 0: outside the class)
+              atomicOr(&aux, (uint32_t)SHX_DUP);  // (verdict 0: outside the class)
           }
         }
-        acc |= st << (2 * side);
+        accb |= st << (2 * side);
       }
-      if (acc) xch.acc[i] = (uint8_t)acc;  // (one byte per event: both sides' owners write it only
-                                           // when they are the same shard, else their bit pairs)
     }
-    if (zw) xch.zw[i] = (uint8_t)zw;
-    s.wlist[k] = i | (roles << 24);
+    // every byte of this shard's copy: its owned facts, zero elsewhere (the sum is the union)
+    xch.zw[i] = (uint8_t)zw;
+    if (XFER) xch.acc[i] = (uint8_t)accb;
+    s.bstatus[i] = (uint8_t)roles;
   }
-  if ((uint64_t)(amount_upper >> 64) != 0) atomicOr(&aux, (uint32_t)SHX_HUGE);
-  {  // owned ids reaching the exists check: one LDS add per wave
-    const uint32_t c = (uint32_t)__popcll(__ballot(owned_id));
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&aux, c << SHX_OWN_SHIFT);
-  }
-  // block sum of the amounts below 2^64: wave sums of the two 64-bit halves, then one LDS word per wave
-  const uint64_t a = ((uint64_t)(amount_upper >> 64) != 0) ? 0ull : (uint64_t)amount_upper;
+  if ((uint64_t)(amount >> 64) != 0) atomicOr(&aux, (uint32_t)SHX_HUGE);
+  // this block's partials: owned ids reaching the exists check (an insert bound), the amounts below 2^64
+  const uint32_t c = (uint32_t)__popcll(__ballot(owned_id));
+  const uint64_t a = ((uint64_t)(amount >> 64) != 0) ? 0ull : (uint64_t)amount;
   u128 v = a;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -450,88 +353,97 @@ __global__ void __launch_bounds__(SEG) k_sh_owned_ct(Dev d, Scratch s, const tb_
     const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(v >> 64), o, 64);
     v += ((u128)hi << 64) | lo;
   }
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = v;
+    if (c) atomicAdd(&aux, c << SHX_OWN_SHIFT);
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {  // this segment's partials (sh_close_fold folds them)
+  if (threadIdx.x == 0) {
     u128 tot = 0;
 #pragma unroll
-    for (int w2 = 0; w2 < SEG / 64; w2++) tot += red[w2];
+    for (int w2 = 0; w2 < SH_SCAN_T / 64; w2++) tot += red[w2];
     s.blk_amt[blockIdx.x] = tot;
-    s.blk_aux[blockIdx.x] |= aux;  // k_sh_roles wrote the segment's prefix bits
+    s.blk_aux[blockIdx.x] = aux;
   }
 }
 
-__global__ void __launch_bounds__(SEG) k_sh_owned_ca(Dev d, Scratch s, const tb_account_t* __restrict__ ev, WinDesc w,
-                                                     uint32_t epoch, XchView xch) {
+// After k_sh_scan, one block: this shard's verdicts into exchange 1's trailer, the window's overflow /
+// prefix / claim state into Globals, this shard's unused mismatch slots zeroed.
+template <bool XFER>
+__global__ void __launch_bounds__(SEG) k_sh_fold(Dev d, Scratch s, uint32_t nblk, XchView xch, uint32_t me) {
+  __shared__ u128 red[SEG / 64];
   __shared__ uint32_t aux;
-  const uint32_t k = blockIdx.x * SEG + threadIdx.x;
-  if (threadIdx.x == 0) aux = 0;
-  if (k == 0) check_window(w, d.g);
-  __syncthreads();
-  const uint32_t n = s.cnt_w[blockIdx.x];
-  if (threadIdx.x < n) {
-    const uint32_t i = ol_event(s.wlist[k]);
-    const tb_account_t a = ev[i];
-    uint32_t cls = 0, roles = 0;
-    bool reach;
-    (void)sh_static_ca(a, &cls, &reach);
-    if (reach) {
-      roles = ROLE_ID;
-      atomicAdd(&aux, 1u << SHX_OWN_SHIFT);
-      bool dup;
-      (void)sh_claim(d.g, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev), a.id, i, w.E, epoch, &dup);
-      if (dup) atomicOr(&aux, (uint32_t)SHX_DUP);
-      AccEntry e;
-      const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, a.id, &e);
-      xch.zw[i] = (uint8_t)(1 + (slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(a, d.acc[slot])));
-    }
-    s.wlist[k] = i | (roles << 24);
+  __shared__ unsigned long long own_s;
+  Globals* g = d.g;
+  const bool claim = !XFER || g->mono_prev == 0;  // (what k_sh_scan read)
+  if (threadIdx.x == 0) {
+    aux = 0;
+    own_s = 0;
   }
   __syncthreads();
-  if (threadIdx.x == 0) s.blk_aux[blockIdx.x] |= aux;
-}
-
-// ------------------------------------------------------------------------------------------------
-// home slice [e0, e1): validation codes, decisions, replies, commit bits.
-// ------------------------------------------------------------------------------------------------
-template <bool XFER>
-__global__ void __launch_bounds__(256) k_sh_home(Scratch s, const uint8_t* __restrict__ ev_bytes, WinDesc w,
-                                                 uint32_t e0, uint32_t e1, uint32_t* trailer2,
-                                                 unsigned long long* bits, uint32_t nwords) {
-  // every commit-bit word of the window starts at zero (k_sh_reply writes this home's words; the
-  // all-reduce sums every shard's): zeroed here rather than by a memset launch
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nwords; k += gridDim.x * blockDim.x) bits[k] = 0;
-  // so do the home segments' failure counts (k_sh_decide adds to them)
-  const uint32_t nseg = (e1 - 1) / SEG - e0 / SEG + 1;
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nseg; k += gridDim.x * blockDim.x) s.cnt_bad[k] = 0;
-  const uint32_t i = e0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= e1) return;
-  const uint32_t b = win_batch(w, i);
-  uint32_t cls = 0, code;
-  bool reach, unsup = false;
+  u128 vt = 0;
+  uint32_t ab = 0;
+  unsigned long long own = 0;
+  for (uint32_t j = threadIdx.x; j < nblk; j += SEG) {
+    const uint32_t x = s.blk_aux[j];
+    ab |= x & 31u;
+    own += x >> SHX_OWN_SHIFT;
+    if (XFER) vt += s.blk_amt[j];
+  }
+  if (ab) atomicOr(&aux, ab);
+  if (own) atomicAdd(&own_s, own);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t lo = __shfl_xor((unsigned long long)(uint64_t)vt, o, 64);
+    const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(vt >> 64), o, 64);
+    vt += ((u128)hi << 64) | lo;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = vt;
+  // this shard's mismatch slots beyond the ones it used are zero in its copy
   if (XFER) {
-    tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
-    code = sh_static_ct(t, w, b, i, &cls, &reach, &unsup);
-  } else {
-    code = sh_static_ca(reinterpret_cast<const tb_account_t*>(ev_bytes)[i], &cls, &reach);
+    const uint32_t used = min(g->sh_mis, SH_MIS_SLOTS);
+    for (uint32_t k = used + threadIdx.x; k < SH_MIS_SLOTS; k += SEG) xch.mis[me * SH_MIS_SLOTS + k] = 0;
   }
-  if (unsup) atomicOr(&trailer2[0], 1u);
-  if (reach) cls |= C_REACH;
-  if (code != CONT) cls |= C_STATIC;
-  s.code[i] = code;
-  s.cls[i] = cls;
-  s.batch[i] = (uint16_t)b;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  u128 tot = 0;
+  for (int w2 = 0; w2 < SEG / 64; w2++) tot += red[w2];
+  const uint32_t bits = aux;
+  uint32_t v0 = (bits & SHX_DUP) ? 1u : 0u, v1 = 0, v2 = 0;
+  const uint32_t v3 = (bits & SHX_UNSUP) ? 1u : 0u;
+  if (XFER) {
+    if ((bits & SHX_NONMONO) && !claim) v0 = 1;  // duplicates were not looked for
+    g->batch_amount_sum += tot;
+    if (bits & SHX_HUGE) g->batch_huge = 1;
+    v1 = g->x_count + own_s > d.x_max ? 1u : 0u;
+    v2 = window_ovf_mode(g) ? 1u : 0u;
+    // every owned balance field stays below 2^64 this window: k_sh_apply's adds need no carry
+    const u128 top = g->ovf_bound + g->batch_amount_sum;
+    g->small_win = (!g->batch_huge && top >= g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1u : 0u;
+    const bool prefix = !(bits & SHX_NONMONO) && (bits & SHX_FRESH) && g->x_sorted == g->x_count;
+    g->win_flags = prefix ? 2u : 0u;
+    g->mono_prev = (bits & SHX_NONMONO) ? 0u : 1u;  // the next window's claim mode (the same on every shard)
+    g->sh_mis = 0;
+  } else {
+    v1 = g->acc_count + own_s > d.acc_max ? 1u : 0u;
+  }
+  g->sh_unsup = 0;  // (k_sh_decide: a committed event reading a balance)
+  xch.trailer[0] = v0 | (v1 << 8) | (v2 << 16) | (v3 << 24);
+  xch.trailer[1] = xch.trailer[2] = xch.trailer[3] = 0;
 }
 
-// An event's code from the exchanged owner facts (its static code first).
+// ------------------------------------------------------------------------------------------------
+// k_sh_decide (after exchange 1): every shard decides every event from the summed facts (2 B per
+// event: the id owner's code, the account sides' states), so no second exchange is needed: account
+// lookups (:1496-1497), ledgers (:1503-1504), exists (:1506-1507), then linked chains (:1240-1300,
+// never across a batch). Per event its commit flag (Scratch::ins); the codes of the home batches'
+// events (replies); per segment the home failures and the committed owned inserts (k_sh_apply's ranks).
+// ------------------------------------------------------------------------------------------------
 template <bool XFER>
-__device__ inline uint32_t sh_code(const Scratch& s, const uint8_t* ev, const XchView& xch, uint32_t j,
-                                   uint32_t* trailer2) {
-  const uint32_t code = s.code[j];
-  if (code != CONT) return code;
+__device__ inline uint32_t sh_code(const XchView& xch, uint32_t j) {
   const uint32_t zw = xch.zw[j];
-  const uint32_t z = (zw & SH_Z_MASK) - 1;
-  if (!XFER) return z;
+  const uint32_t z = (zw & ZW_CODE) - 1;
+  if (!XFER || (zw & ZW_STATIC)) return z;
   const uint32_t acc = xch.acc[j], dst = acc & 3u, cst = (acc >> 2) & 3u;
   if (dst == SH_ACC_MISSING) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;  // :1496-1497
   if (cst == SH_ACC_MISSING) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
@@ -542,210 +454,211 @@ __device__ inline uint32_t sh_code(const Scratch& s, const uint8_t* ev, const Xc
     if (xch_mis_ledger(xch, j, 0) != xch_mis_ledger(xch, j, 1)) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
     return TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
   }
-  if (z != TB_CT_OK) return z;  // exists* (:1506-1507)
-  // Reaches the balance checks: overflow cannot fail in a class window; a limit flag on either
-  // account is a balance read (:1546-1547), and flags.history a row of balances after the event
-  // (:1806-1841): outside the class.
-  if (zw & (SH_DR_LIMIT | SH_CR_LIMIT)) atomicOr(&trailer2[0], 1u);
-  return TB_CT_OK;
+  return z;  // exists* or ok (:1506-1507)
 }
 
 template <bool XFER>
-__global__ void __launch_bounds__(256) k_sh_decide(Scratch s, const uint8_t* ev, WinDesc w, uint32_t e0, uint32_t e1,
-                                                   XchView xch, uint32_t* trailer2) {
-  const uint32_t i = e0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= e1) return;
-  const uint32_t b = s.batch[i];
-  const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
-  if (i != first && (s.cls[i - 1] & C_LINKED)) return;  // chain member: its head decides
-  const uint32_t cls = s.cls[i];
-  const uint32_t k0 = e0 / SEG;  // failures per home segment (s.cnt_bad[seg - k0]: k_sh_reply's ranks)
-  if (!(cls & C_LINKED)) {
-    const uint32_t code = sh_code<XFER>(s, ev, xch, i, trailer2);
-    s.code[i] = code;
-    if (code == TB_CT_OK) s.cls[i] = cls | C_COMMIT;
-    else atomicAdd(&s.cnt_bad[i / SEG - k0], 1u);
-    return;
-  }
-  // chain head: members i..end (:1240-1300). No member's outcome depends on another member's
-  // effects in a class window, so the chain fails at its first failing member.
-  uint32_t end = i, f = NONE32;
-  for (uint32_t j = i;; j++) {
-    const bool lj = s.cls[j] & C_LINKED;
-    uint32_t code = sh_code<XFER>(s, ev, xch, j, trailer2);
-    if (lj && j == last) code = TB_CT_LINKED_EVENT_CHAIN_OPEN;  // :1247
-    s.code[j] = code;
-    if (code != TB_CT_OK && f == NONE32) f = j;
-    end = j;
-    if (!lj || j == last) break;
-  }
-  for (uint32_t j = i; j <= end; j++) {
-    const uint32_t cj = s.cls[j];
-    if (f == NONE32) {
-      s.cls[j] = cj | C_COMMIT;
-    } else if (j != f && !((cj & C_LINKED) && j == last)) {
-      s.code[j] = TB_CT_LINKED_EVENT_FAILED;  // back-fill before f, broken chain after f
+__global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes, WinDesc w,
+                                                   XchView xch, uint32_t e0, uint32_t e1) {
+  __shared__ uint32_t nbad, nins;
+  __shared__ u128 ldsm[SEG / 64];
+  Globals* g = d.g;
+  if (sh_verdict(xch)) return;  // outside the class: k_sh_apply reports it
+  if (blockIdx.x == 0 && threadIdx.x == 0) g->base = XFER ? g->x_count : g->acc_count;  // k_sh_apply's insert base
+  if (threadIdx.x == 0) nbad = nins = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * SEG + threadIdx.x, seg = blockIdx.x;
+  uint32_t lbad = 0, lins = 0;
+  u128 idm = 0;  // the largest id this block's chains insert (exact x_id_max: k_sh_apply folds them)
+  if (i < w.E) {
+    const uint32_t b = win_batch(w, i);
+    const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
+    const bool head = i == first || !(xch.zw[i - 1] & ZW_LINKED);
+    if (head) {
+      // a single event, or the head of a chain i..end: no member's outcome depends on another member's
+      // effects in a class window, so the chain fails at its first failing member
+      uint32_t end = i, f = NONE32;
+      for (uint32_t j = i;; j++) {
+        const bool lj = xch.zw[j] & ZW_LINKED;
+        uint32_t code = sh_code<XFER>(xch, j);
+        if (lj && j == last) code = XFER ? (uint32_t)TB_CT_LINKED_EVENT_CHAIN_OPEN : (uint32_t)TB_CA_LINKED_EVENT_CHAIN_OPEN;
+        if (j >= e0 && j < e1) s.code[j] = code;
+        // a committed event reading a balance (limit) or writing a history row: outside the class
+        if (XFER && code == TB_CT_OK && (xch.acc[j] & (ACC_DR_LIMIT | ACC_CR_LIMIT))) atomicOr(&g->sh_unsup, 1u);
+        if (code != TB_CT_OK && f == NONE32) f = j;
+        end = j;
+        if (!lj || j == last) break;
+      }
+      for (uint32_t j = i; j <= end; j++) {
+        const bool commit = f == NONE32;
+        if (!commit && j != f && j >= e0 && j < e1 && !((xch.zw[j] & ZW_LINKED) && j == last))
+          s.code[j] = XFER ? (uint32_t)TB_CT_LINKED_EVENT_FAILED : (uint32_t)TB_CA_LINKED_EVENT_FAILED;
+        s.ins[j] = commit ? 1 : 0;
+        const uint32_t bad = (!commit && j >= e0 && j < e1) ? 1u : 0u;
+        const uint32_t ins = (commit && (s.bstatus[j] & ROLE_ID)) ? 1u : 0u;
+        if (XFER && ins) idm = umax128(idm, U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[j].id));
+        if (j / SEG == seg) {
+          lbad += bad;
+          lins += ins;
+        } else {  // (a chain running into the next segment)
+          if (bad) atomicAdd(&s.cnt_bad[j / SEG], 1u);
+          if (ins) atomicAdd(&s.cnt_ins[j / SEG], 1u);
+        }
+      }
     }
   }
-  if (f != NONE32) {  // every member failed; the chain may span several segments
-    for (uint32_t g = i / SEG; g <= end / SEG; g++)
-      atomicAdd(&s.cnt_bad[g - k0], std::min(end + 1, (g + 1) * SEG) - std::max(i, g * SEG));
+  const uint32_t wb = wave_sum(lbad), wi = wave_sum(lins);
+  if (XFER) idm = wave_max_u128(idm);
+  if ((threadIdx.x & 63) == 0) {
+    if (wb) atomicAdd(&nbad, wb);
+    if (wi) atomicAdd(&nins, wi);
+    if (XFER) ldsm[threadIdx.x >> 6] = idm;
   }
-}
-
-// Home slice: replies of batches [hb0, hb1) (batch_base relative to hb0, indices batch-relative) and
-// the commit bit of every slice event (one 64-bit word per wave; words are window-aligned).
-__global__ void __launch_bounds__(SEG) k_sh_reply(Dev d, Scratch s, WinDesc w, uint32_t hb0, uint32_t hb1, uint32_t e0,
-                                                  uint32_t e1, uint32_t k0, FinalOut o, unsigned long long* bits,
-                                                  const uint32_t* unsup, uint32_t* trailer2, uint32_t nscan,
-                                                  uint32_t xfer) {
-  __shared__ uint32_t lds[SEG / 64];
-  __shared__ u128 red[SEG / 64];
-  __shared__ uint32_t bits_s;
-  __shared__ unsigned long long own_s;
-  if (blockIdx.x == 0) {  // (block-uniform) exchange 2's trailer, instead of a memset before the homes
-    const uint32_t verdict = sh_close_fold(d, s, nscan, xfer, red, &bits_s, &own_s);
-    if (threadIdx.x == 0) sh_trailer2(trailer2, *unsup, verdict);
-  }
-  const uint32_t i = (k0 + blockIdx.x) * SEG + threadIdx.x;
-  const bool mine = i >= e0 && i < e1;
-  uint32_t cls = 0, code = TB_CT_OK;
-  if (mine) {
-    cls = s.cls[i];
-    code = s.code[i];
-  }
-  const uint32_t bad = code != TB_CT_OK;
-  const uint32_t pbad = seg_prefix<SEG>(s.cnt_bad, blockIdx.x, lds);
-  uint32_t tot_bad;
-  const uint32_t rbad = pbad + block_excl<SEG / 64>(bad, lds, &tot_bad);
-  const unsigned long long m = __ballot(mine && (cls & C_COMMIT));
-  if ((threadIdx.x & 63) == 0 && i < e1 && i + 64 > e0) bits[i / 64] = m;
-  if (!mine) return;
-  const uint32_t b = s.batch[i];
-  if (i == w.off[b]) {
-    // event i opens batch b and every empty home batch just before it
-    for (int32_t bb = (int32_t)b; bb >= (int32_t)hb0 && w.off[bb] == i; bb--) o.batch_base[bb - hb0] = rbad;
-  }
-  if (bad && sh_guard(d.g, rbad < e1 - e0, 2, rbad)) {
-    tb_create_result_t r;
-    r.index = i - w.off[b];
-    r.result = code;
-    o.results[rbad] = r;
-  }
-  if (i == e1 - 1) {
-    const uint32_t total_bad = rbad + bad;
-    for (int32_t bb = (int32_t)hb1; bb >= (int32_t)hb0 && w.off[bb] == e1; bb--) o.batch_base[bb - hb0] = total_bad;
-    if (o.out_count) *o.out_count = total_bad;
-    d.g->result_count = total_bad;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (nbad) atomicAdd(&s.cnt_bad[seg], nbad);
+    if (nins) atomicAdd(&s.cnt_ins[seg], nins);
+    if (XFER) {
+      u128 bm = ldsm[0];
+      for (int q = 1; q < SEG / 64; q++) bm = umax128(bm, ldsm[q]);
+      s.blk_idmax[seg] = bm;
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// apply: whole window, owned roles of committed events.
+// k_sh_apply: the home batches' replies (batch_base relative to hb0, indices batch-relative), then the
+// owned effects of the committed events: the account owners add the amounts (no-return 64-bit adds
+// when the window keeps every balance field below 2^64, else exact 128-bit atomics), the id owner
+// appends the record in event order (sorted prefix when the window's ids rise above every stored id)
+// and indexes it. The last block folds the inserted ids' exact maximum and closes the window. A window outside the class (exchange 1's verdict, or a committed event reading a balance)
+// changes nothing on any shard: window_error bit 1 (TBG_E_UNSUPPORTED at tbg_sync).
 // ------------------------------------------------------------------------------------------------
-__device__ inline bool sh_bit(const unsigned long long* bits, uint32_t i) { return (bits[i / 64] >> (i & 63)) & 1ull; }
+__device__ inline bool sh_abort(const XchView& x, const Globals* g) { return sh_verdict(x) || g->sh_unsup != 0; }
 
-// Verdict of the window, identical on every shard: exchange 2's trailer (homes: an event outside the
-// class; owners: duplicate id, capacity, overflow bound).
-__device__ inline bool sh_abort(const uint32_t* trailer2) {
-  return (trailer2[0] | trailer2[1] | trailer2[2] | trailer2[3]) != 0;
-}
-
-// Per segment: committed owned-id entries (insert counts), over the segment lists.
-__global__ void __launch_bounds__(SEG) k_sh_icount(Dev d, Scratch s, uint32_t xfer, const unsigned long long* bits) {
-  __shared__ uint32_t lds[SEG / 64];
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.g->base = xfer ? d.g->x_count : d.g->acc_count;  // k_sh_apply's base
-  uint32_t ins = 0;
-  if (threadIdx.x < s.cnt_w[blockIdx.x]) {
-    const uint32_t x = s.wlist[blockIdx.x * SEG + threadIdx.x];
-    ins = ((ol_roles(x) & ROLE_ID) && sh_bit(bits, ol_event(x))) ? 1u : 0u;
-  }
-  const uint32_t tot = block_sum<SEG / 64>(ins, lds);
-  if (threadIdx.x == 0) s.cnt_ins[blockIdx.x] = tot;
-}
-
-template <bool XFER>
-__global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w,
-                                                  const uint32_t* trailer2, const unsigned long long* bits,
+// STAGE (one shard: every event is owned, the inserts are dense): a wave's inserted records are
+// compacted in LDS and stored as one contiguous run (as in k_final); with several shards the inserts
+// are sparse and each inserting lane stores its record whole (no 128 KiB of LDS: twice the resident
+// blocks).
+template <bool XFER, bool STAGE>
+__global__ void __launch_bounds__(SEG) __attribute__((amdgpu_waves_per_eu(STAGE ? 4 : 8))) k_sh_apply(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w, XchView xch,
+                                                  uint32_t hb0, uint32_t hb1, uint32_t e0, uint32_t e1, FinalOut o,
                                                   ChgLog chg, uint32_t chg_epoch) {
   __shared__ uint32_t lds[SEG / 64];
   __shared__ u128 ldsm[SEG / 64];
-  // inserted transfer records, compacted per wave and stored as one contiguous run (as in k_final)
-  __shared__ uint4 stage[XFER ? SEG * 8 : 1];
+  __shared__ uint4 stage[XFER && STAGE ? SEG * 8 : 1];
   Globals* g = d.g;
-  const bool last_block = blockIdx.x == gridDim.x - 1;
-  if (sh_abort(trailer2)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&g->window_error, 2u);
-    if (last_block && threadIdx.x == 0) sh_window_reset(g, XFER, 0, false);
+  if (sh_abort(xch, g)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      atomicOr(&g->window_error, 2u);
+      sh_window_reset(g, XFER, 0, false);
+    }
     return;
   }
-  const bool prefix_win = XFER && (g->win_flags & 2u) != 0;  // sh_close_fold
-  const bool small = XFER && g->small_win != 0;              // sh_close_fold
-  const uint64_t xbase = g->base;  // captured by k_sh_icount: the last block rewrites the count
-  const uint32_t n = s.cnt_w[blockIdx.x];
-  uint32_t i = 0, roles = 0;
-  bool commit = false;
-  if (threadIdx.x < n) {
-    const uint32_t x = s.wlist[blockIdx.x * SEG + threadIdx.x];
-    i = ol_event(x);
-    roles = ol_roles(x);
-    commit = roles && sh_bit(bits, i);
+  const bool prefix_win = XFER && (g->win_flags & 2u) != 0;  // k_sh_scan
+  const bool small = XFER && g->small_win != 0;              // k_sh_scan
+  const uint64_t xbase = g->base;                            // k_sh_decide
+  const uint32_t i = blockIdx.x * SEG + threadIdx.x;
+  const bool in = i < w.E;
+  const bool commit = in && s.ins[i];
+  const uint32_t roles = in ? s.bstatus[i] : 0u;
+  // ---- replies of the home batches ----
+  const bool home = i >= e0 && i < e1;
+  const uint32_t code = home ? s.code[i] : (uint32_t)TB_CT_OK;
+  const uint32_t bad = home && code != TB_CT_OK ? 1u : 0u;
+  uint32_t tot;
+  const uint32_t rbad = seg_prefix<SEG>(s.cnt_bad, blockIdx.x, lds) + block_excl<SEG / 64>(bad, lds, &tot);
+  if (home) {
+    const uint32_t b = win_batch(w, i);
+    if (i == w.off[b]) {
+      // event i opens batch b and every empty home batch just before it
+      for (int32_t bb = (int32_t)b; bb >= (int32_t)hb0 && w.off[bb] == i; bb--) o.batch_base[bb - hb0] = rbad;
+    }
+    if (bad && sh_guard(g, rbad < e1 - e0, 2, rbad)) {
+      tb_create_result_t r;
+      r.index = i - w.off[b];
+      r.result = code;
+      o.results[rbad] = r;
+    }
+    if (i == e1 - 1) {
+      const uint32_t total_bad = rbad + bad;
+      for (int32_t bb = (int32_t)hb1; bb >= (int32_t)hb0 && w.off[bb] == e1; bb--) o.batch_base[bb - hb0] = total_bad;
+      if (o.out_count) *o.out_count = total_bad;
+      g->result_count = total_bad;
+    }
   }
+  // ---- owned effects ----
   bool ins = commit && (roles & ROLE_ID);
   const uint32_t pins = seg_prefix<SEG>(s.cnt_ins, blockIdx.x, lds);
   uint32_t tot_ins;
   const uint32_t rins = pins + block_excl<SEG / 64>(ins ? 1u : 0u, lds, &tot_ins);
-  if (XFER) {
-    const u128 key = ins ? U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].id) : (u128)0;
-    const u128 m = wave_max_u128(key);
-    if ((threadIdx.x & 63) == 0) ldsm[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      u128 bm = ldsm[0];
-      for (int q = 1; q < SEG / 64; q++) bm = umax128(bm, ldsm[q]);
-      if (bm > g->x_id_max) atomic_bound_u128(&g->x_id_max, bm);
-    }
-  }
-  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, 0);  // the wave's first insert rank (all lanes active here)
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, 0);  // the wave's first insert rank
   if (commit) {
     if (XFER) {
       uint32_t drs = (roles & ROLE_DR) ? s.dr_slot[i] : NONE32, crs = (roles & ROLE_CR) ? s.cr_slot[i] : NONE32;
       if (drs != NONE32 && !sh_guard(g, drs < d.acc_max, 3, drs)) drs = NONE32;
       if (crs != NONE32 && !sh_guard(g, crs < d.acc_max, 4, crs)) crs = NONE32;
       if (ins && !sh_guard(g, xbase + rins < d.x_max, 5, xbase + rins)) ins = false;
-      const u128 a = U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i].amount);
+      const tb_transfer_t* t = reinterpret_cast<const tb_transfer_t*>(ev_bytes) + i;
       Add128 a_dr, a_cr;
-      if (drs != NONE32) a_dr.issue(&d.acc[drs].debits_posted, a, small);
-      if (crs != NONE32) a_cr.issue(&d.acc[crs].credits_posted, a, small);
-      if (chg.mark) {  // write-back stream (changes.h): the owned accounts this window changed
-        if (drs != NONE32) chg.mark[drs] = chg_epoch;
-        if (crs != NONE32) chg.mark[crs] = chg_epoch;
+      if (drs != NONE32 || crs != NONE32) {
+        const u128 a = U(t->amount);
+        if (drs != NONE32) a_dr.issue(&d.acc[drs].debits_posted, a, small);
+        if (crs != NONE32) a_cr.issue(&d.acc[crs].credits_posted, a, small);
+        if (chg.mark) {  // write-back stream (changes.h): the owned accounts this window changed
+          if (drs != NONE32) chg.mark[drs] = chg_epoch;
+          if (crs != NONE32) chg.mark[crs] = chg_epoch;
+        }
       }
       if (ins) {
         const uint64_t slot = xbase + rins;
-        tb_transfer_t t2 = reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i];
-        t2.timestamp = win_ts(w, win_batch(w, i), i);
-        // ranks of a wave's inserts are consecutive (block_excl); a failed slot guard can only drop
-        // a suffix of them, so the staged run below stays gap-free
-        const uint4* tw = reinterpret_cast<const uint4*>(&t2);
-        uint4* ws = stage + (threadIdx.x >> 6) * 512;
+        const uint64_t ts = win_ts(w, win_batch(w, i), i);
+        // the record as 16 B words, in two halves (a whole record in registers costs 32 VGPRs)
+        const uint4* src = reinterpret_cast<const uint4*>(t);
+        uint4* ws = stage + (threadIdx.x >> 6) * 512 + (rins - r0) * 8;
+        uint4* dst = reinterpret_cast<uint4*>(d.xr + slot);
+        tb_uint128_t id;
 #pragma unroll
-        for (int q = 0; q < 8; q++) ws[(rins - r0) * 8 + q] = tw[q];
-        if (!prefix_win) x_insert(d.x_tab, d.x_mask, t2.id, (uint32_t)slot);
+        for (int half = 0; half < 2; half++) {
+          uint4 r[4];
+#pragma unroll
+          for (int q = 0; q < 4; q++) r[q] = src[half * 4 + q];
+          if (half == 0) id = rw_u128(r[0]);
+          else {
+            r[3].z = (uint32_t)ts;  // the stamped timestamp (word 7)
+            r[3].w = (uint32_t)(ts >> 32);
+          }
+          // ranks of a wave's inserts are consecutive (block_excl); a failed slot guard can only drop
+          // a suffix of them, so the staged run below stays gap-free
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            if (STAGE)
+              ws[half * 4 + q] = r[q];
+            else
+              st_stream(dst + half * 4 + q, r[q]);
+          }
+        }
+        if (!prefix_win) x_insert(d.x_tab, d.x_mask, id, (uint32_t)slot);
         d.xstatus[slot] = 0;
       }
       a_dr.finish();
       a_cr.finish();
     } else if (ins && sh_guard(g, xbase + rins < d.acc_max, 6, xbase + rins)) {
+      // (the record as 16 B words: a struct copy whose address is taken goes to scratch memory)
       const uint64_t slot = xbase + rins;
-      tb_account_t a = reinterpret_cast<const tb_account_t*>(ev_bytes)[i];
-      a.timestamp = win_ts(w, win_batch(w, i), i);
-      d.acc[slot] = a;
+      const uint4* src = reinterpret_cast<const uint4*>(ev_bytes) + (size_t)i * 8;
+      uint4 r[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) r[q] = src[q];
+      rw_stamp(r, win_ts(w, win_batch(w, i), i));
+      uint4* dst = reinterpret_cast<uint4*>(d.acc + slot);
+#pragma unroll
+      for (int q = 0; q < 8; q++) dst[q] = r[q];
       d.hot[slot] = 0;
-      acc_insert(d.acc_tab, d.acc_mask, a.id, (uint32_t)slot, a.ledger, a.flags);
+      acc_insert(d.acc_tab, d.acc_mask, rw_u128(r[0]), (uint32_t)slot, r[7].x, (uint16_t)(r[7].y >> 16));
     }
   }
-  if (XFER) {
+  if (XFER && STAGE) {
     const uint32_t nins = (uint32_t)__popcll(__ballot(ins));
     wave_sync();
     if (nins) {
@@ -754,8 +667,24 @@ __global__ void __launch_bounds__(SEG) k_sh_apply(Dev d, Scratch s, const uint8_
       for (uint32_t k = threadIdx.x & 63; k < nins * 8; k += 64) st_stream(dst + k, ws[k]);
     }
   }
-  if (last_block && threadIdx.x == 0) {
-    const uint64_t total = xbase + pins + tot_ins;
+  // The last block (by index; the others may still run: they read Globals::base, captured by
+  // k_sh_decide, never the counts written here) closes the window from k_sh_decide's per-segment
+  // counts and exact per-segment id maxima.
+  if (blockIdx.x != gridDim.x - 1) return;
+  const uint32_t total_ins = pins + tot_ins;
+  u128 mx = 0;
+  if (XFER) {
+    for (uint32_t j = threadIdx.x; j < gridDim.x; j += SEG) mx = umax128(mx, s.blk_idmax[j]);
+    mx = wave_max_u128(mx);
+    if ((threadIdx.x & 63) == 0) ldsm[threadIdx.x >> 6] = mx;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (XFER) {
+      for (int q = 0; q < SEG / 64; q++) mx = umax128(mx, ldsm[q]);
+      if (mx > g->x_id_max) g->x_id_max = mx;
+    }
+    const uint64_t total = xbase + total_ins;
     g->events_total += w.E;
     if (prefix_win) g->x_sorted = total;
     sh_window_reset(g, XFER, total, true);

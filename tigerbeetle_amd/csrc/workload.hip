@@ -420,3 +420,21 @@ extern "C" int tbg_gen_permute_ids(void* d_records, uint64_t count, uint32_t tra
                                                                                 transfers, order, seed);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+// Mixed streams: every `every`-th generated transfer (global index first + k with (first + k) % every ==
+// every - 1) becomes a pending create (flags.pending, timeout `timeout` seconds); the rest are untouched.
+__global__ void k_mark_pending(uint8_t* recs, uint64_t first, uint64_t count, uint64_t every, uint32_t timeout) {
+  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (k >= count || (first + k) % every != every - 1) return;
+  uint8_t* r = recs + k * 128;
+  *reinterpret_cast<uint32_t*>(r + 108) = timeout;
+  *reinterpret_cast<uint16_t*>(r + 118) |= (uint16_t)(1u << 1);
+}
+
+extern "C" int tbg_gen_mark_pending(void* d_records, uint64_t first, uint64_t count, uint64_t every, uint32_t timeout,
+                                    void* stream) {
+  if (!count || !every) return 0;
+  k_mark_pending<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>((uint8_t*)d_records, first, count,
+                                                                                 every, timeout);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

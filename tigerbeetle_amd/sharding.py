@@ -3,17 +3,16 @@
 Account a lives on shard `shard_of(a.id)`, transfer t on shard `shard_of(t.id)` (csrc/shard.h).
 Every shard receives the same prepared window (the replica hands each GPU the same prepare body,
 state_machine.zig:1107-1146) and is the home of a contiguous range of its batches (`home_range`).
-A window commits in five steps through the C ABI (include/tbg.h):
+A window commits in three steps through the C ABI (include/tbg.h):
 
-  tbg_shard_prepare_window   owned roles only: validate, resolve the owned accounts / ids, write the
-                             owner facts (9 B per transfer: debit / credit ledger, exists code +
-                             limit bits; one writer per bit)
+  tbg_shard_prepare_window   one pass over the window: the owners validate and resolve what they own
+                             (accounts, ids) and write the owner facts (2 B per transfer: the id
+                             owner's code, the account sides' states; one writer per bit)
   exchange                   byte-wise sum of the facts across the shards, on the engine's stream
                              (RCCL uint8 all-reduce over xGMI: torch "nccl")
-  tbg_shard_decide_window    home batches only: decide, write their replies and one commit bit per
-                             event
-  exchange                   byte-wise sum of the commit bits (E/8 B) across the shards
-  tbg_shard_commit_window    owned effects of the committed events
+  tbg_shard_commit_window    every shard decides every event from the facts (the same outcome
+                             everywhere: no second exchange), writes its home batches' replies and
+                             applies the owned effects of the committed events
 
 The `exchange` callable is the only collective on the data path; with one shard there is none.
 Per shard, the work is the window's ids plus 1/G of the rest: it falls as G grows.
@@ -131,7 +130,6 @@ class ShardedStateMachine:
         xb = max(L.tbg_shard_exchange_bytes(int(op), events_max, shard_count)
                  for op in (Operation.create_accounts, Operation.create_transfers))
         self.xch = torch.zeros(int(xb), dtype=torch.uint8, device=dev)
-        self.bits = torch.zeros(int(_lib.lib().tbg_shard_commit_bits_bytes(events_max)), dtype=torch.uint8, device=dev)
         self.stream = torch.cuda.ExternalStream(self.sm.stream, device=dev)
         self._n_events = 0
         self._pulse_next = None  # cached pulse_next_timestamp (order-free windows never change it)
@@ -170,17 +168,10 @@ class ShardedStateMachine:
         n = _lib.lib().tbg_shard_exchange_bytes(int(operation), self._n_events, self.shard_count)
         return self.xch[:n]
 
-    def decide_window(self, home_first, home_count, d_results, d_batch_base):
-        """Step 3 (after the facts were summed); returns the commit-bit tensor to be summed."""
-        _lib.check(_lib.lib().tbg_shard_decide_window(self.sm.h, self.xch.data_ptr(), home_first, home_count,
-                                                      d_results, d_batch_base, self.bits.data_ptr()),
-                   "shard_decide_window")
-        return self.bits[:_lib.lib().tbg_shard_commit_bits_bytes(self._n_events)]
-
-    def commit_decided(self):
-        """Step 5 (after the commit bits were summed)."""
-        _lib.check(_lib.lib().tbg_shard_commit_window(self.sm.h, self.xch.data_ptr(), self.bits.data_ptr()),
-                   "shard_commit_window")
+    def commit_prepared(self, home_first, home_count, d_results, d_batch_base):
+        """Step 3 (after the facts were summed): decide, reply for the home batches, apply."""
+        _lib.check(_lib.lib().tbg_shard_commit_window(self.sm.h, self.xch.data_ptr(), home_first, home_count,
+                                                      d_results, d_batch_base), "shard_commit_window")
 
     def commit_window(self, operation, d_events, batch_events, batch_timestamps, d_results, d_batch_base):
         """Asynchronous on the engine stream (after the harness pulse before the first batch, when
@@ -196,11 +187,7 @@ class ShardedStateMachine:
         if self.exchange is not None:
             with torch.cuda.stream(self.stream):
                 self.exchange(words)
-        bits = self.decide_window(first, count, d_results, d_batch_base)
-        if self.exchange is not None:
-            with torch.cuda.stream(self.stream):
-                self.exchange(bits)
-        self.commit_decided()
+        self.commit_prepared(first, count, d_results, d_batch_base)
         return first, count
 
     def sync(self):

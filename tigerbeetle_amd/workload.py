@@ -289,3 +289,14 @@ def permute_ids(recs, order, seed=0):
         recs[f + "_lo"] = np.where(m, elo, lo)
         recs[f + "_hi"] = np.where(m, ehi, hi)
     return recs
+
+
+def mark_pending(recs, first, every, timeout):
+    """Numpy twin of tbg_gen_mark_pending: transfer (first + k) with (first + k) % every == every - 1
+    becomes a pending create with `timeout` seconds."""
+    if every:
+        k = np.arange(first, first + len(recs), dtype=np.uint64)
+        m = k % np.uint64(every) == np.uint64(every - 1)
+        recs["timeout"][m] = timeout
+        recs["flags"][m] |= np.uint16(1 << 1)
+    return recs

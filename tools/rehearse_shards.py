@@ -1,14 +1,14 @@
 """Per-shard GPU time of the hash-sharded commit at G shards, rehearsed on ONE GPU.
 
 G ShardedStateMachine engines live on cuda:0 in this process. Each window runs shard by shard
-(prepare -> in-process byte-wise sum of the facts, i.e. what the RCCL all-reduce computes -> decide
-(home batches) -> sum of the commit bits -> commit), with HIP events on each engine's stream around
-each step. A shard's GPU time per window is what one GPU of a G-GPU node spends on the window apart
-from the collectives, so
+(prepare -> in-process byte-wise sum of the facts, i.e. what the RCCL all-reduce computes -> commit:
+decide every event, reply for the home batches, apply the owned effects), with HIP events on each
+engine's stream around each step. A shard's GPU time per window is what one GPU of a G-GPU node
+spends on the window apart from the collective, so
 
-    estimated G-GPU rate = global events / sum over windows of max over shards (prep + decide + commit)
+    estimated G-GPU rate = global events / sum over windows of max over shards (prepare + commit)
 
-is an upper bound for the real node (the all-reduces of 9 B + 1 bit per event are added on top).
+is an upper bound for the real node (the all-reduce of 2 B per event is added on top).
 Not a bench line: evidence for DESIGN.md §7. Usage (on the GPU box):
 
     python tools/rehearse_shards.py --shards 8 --accounts 2000000 --transfers 40000000 --window 64
@@ -215,15 +215,12 @@ def main():
             pulse_general(shards, summed, ts[0])
         words, ev1 = timed_step(lambda r, s: s.prepare_window(op, ptr, ns, ts))
         summed(words)
-        bits, ev2 = timed_step(lambda r, s: s.decide_window(*s.home_range(len(ns)), d_res.data_ptr(),
-                                                            d_base.data_ptr() + r * 256 * 4))
-        summed(bits)
-        _, ev3 = timed_step(lambda r, s: s.commit_decided())
+        _, ev2 = timed_step(lambda r, s: s.commit_prepared(*s.home_range(len(ns)), d_res.data_ptr(),
+                                                           d_base.data_ptr() + r * 256 * 4))
         for s in shards:
             s.sync()
         if timed:
-            times.append([(a[0].elapsed_time(a[1]), b_[0].elapsed_time(b_[1]), c[0].elapsed_time(c[1]))
-                          for a, b_, c in zip(ev1, ev2, ev3)])
+            times.append([(a[0].elapsed_time(a[1]), b_[0].elapsed_time(b_[1])) for a, b_ in zip(ev1, ev2)])
         return sum(ns)
 
     nb_acc = (n_acc + BATCH - 1) // BATCH
@@ -235,17 +232,16 @@ def main():
         n = window(Operation.create_transfers, d_x, b0, min(b0 + win, nb), n_x, k >= a.warmup)
         if k >= a.warmup:
             events += n
-    t = np.array(times)  # windows x shards x (prep, decide, commit), ms
+    t = np.array(times)  # windows x shards x (scan, decide + apply), ms
     per_shard = t.sum(axis=2)
     crit = per_shard.max(axis=1).sum() / 1000.0
     out = {
         "shards": G, "window_batches": win, "timed_windows": len(times), "events_timed": events,
-        "shard_ms_per_window": {"prep_mean": round(float(t[:, :, 0].mean()), 4),
-                                "decide_mean": round(float(t[:, :, 1].mean()), 4),
-                                "commit_mean": round(float(t[:, :, 2].mean()), 4),
+        "shard_ms_per_window": {"scan_mean": round(float(t[:, :, 0].mean()), 4),
+                                "decide_apply_mean": round(float(t[:, :, 1].mean()), 4),
                                 "max_shard_mean": round(float(per_shard.max(axis=1).mean()), 4)},
         "estimated_rate_excl_collective": round(events / crit, 1),
-        "exchange_bytes_per_window": (16 + 2 * win * BATCH + 8 * G * 4096) + 16 + win * BATCH // 8,
+        "exchange_bytes_per_window": 16 + 2 * win * BATCH + 8 * G * 4096,
         "stats_shard0": shards[0].stats(),
     }
     print(json.dumps(out), flush=True)

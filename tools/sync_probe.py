@@ -48,7 +48,8 @@ def main():
             sm.prepare_timestamp += 1 + BATCH
             T = sm.prepare_timestamp
             x0 = time.perf_counter()
-            assert not sm.pulse()
+            if sm.pulse():
+                sm.commit(0, 1, T, Operation.pulse, b"")
             x1 = time.perf_counter()
             sm.prefetch_timestamp = T
             sm.prefetch(2, Operation.create_transfers, b)
@@ -76,6 +77,8 @@ def main():
         ptr = b.ctypes.data
         x0 = time.perf_counter()
         L.tbg_pulse_needed(h, T, ctypes.byref(need))
+        if need.value:
+            L.tbg_commit(h, 1, T, int(Operation.pulse), None, 0, res.ctypes.data, res.size, ctypes.byref(n_out))
         x1 = time.perf_counter()
         L.tbg_prefetch(h, 2, int(Operation.create_transfers), ptr, BATCH * 128, T)
         x2 = time.perf_counter()
