@@ -549,7 +549,8 @@ def run_sharded(args, torch, dist, world, rank, device):
                     "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
                     "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
                     "phase_avg_us_warmup": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
-                    "exchange_bytes_per_window_per_gpu": 16 + 2 * win * BATCH + 8 * G * 4096}
+                    "exchange_bytes_per_window_per_gpu": int(L.tbg_shard_exchange_bytes(
+                        int(Operation.create_transfers), win * BATCH, G))}
         line = {
             "metric": "committed transfers/sec (create_transfers)",
             "value": round(timed_events / elapsed, 1),

@@ -142,14 +142,19 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t fu_epoch;    // the window k_ct_fused ran for (not backed off)
   uint32_t fu_prefix;   // that window extends the sorted prefix (captured before k_fu_final updates it)
   uint64_t fu_base;     // that window's first record slot
-  uint64_t fu_bad;      // that window's failures: [63:32] epoch | [31:0] count
+  uint64_t pad7;
   uint64_t fu_windows;  // cumulative windows committed by the fused pass
   uint32_t fu_fail_epoch;  // the fused-only window that left the class (window_error bit 3)
   uint32_t sh_mis;         // sharded: this shard's ledger-mismatch slots used this window (shard.h)
   uint32_t sh_unsup;       // sharded: a home event outside the class this window (k_sh_reply -> trailer 2)
   uint64_t ovf_rescans;    // times ovf_bound was re-tightened to the accounts' largest balance sum (restore.h)
   uint32_t fu_nonmono;     // the epoch of a fused window whose ids did not all rise (claim mode, fused.h)
-  uint32_t sh_done;        // sharded: blocks of k_sh_scan / k_sh_apply finished (the last one folds, shard.h)
+  uint32_t pad6;
+  // fused pass: exp_count as k_ct_fused saw it; the window's live expiry entries go after it
+  // (reserved per block in FuScratch::slots, written by k_fu_final)
+  uint64_t fu_exp_base;
+  uint32_t sh_cap_bad;  // sharded order-free window: some shard's store lacks room for its inserts (k_sh_decide)
+  uint32_t pad8;
 };
 
 // The fused pass (fused.h) committed this window: the general path's kernels return at once.

@@ -1655,6 +1655,25 @@ __global__ void __launch_bounds__(LOOKUP_THREADS) k_lookup(Dev d, const tb_uint1
 __global__ void k_init_globals(Globals* g, Globals v) { *g = v; }
 __global__ void k_clear_bits(uint32_t* p, uint32_t bits) { atomicAnd(p, ~bits); }
 
+// The synchronous path's host <-> device bytes as kernels on the engine stream (host.inc
+// stage_request, reply_out), reading and writing pinned host memory through its device mapping: a
+// copy-engine transfer waits ~10 us for the compute queue on each side of it (measured,
+// DESIGN.md §5), more than the transfer of a whole 1 MiB request.
+__global__ void __launch_bounds__(256) k_copy_in(uint4* __restrict__ dst, const uint4* __restrict__ src, uint32_t n16) {
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n16; k += gridDim.x * 256) dst[k] = src[k];
+}
+// The Globals ([0, g16) words) and, with the reply, the reply block at H_REPLY_OFF (its count and the
+// first min(count, n_max) results): the same layout on both sides.
+__global__ void __launch_bounds__(256) k_reply_out(const uint4* __restrict__ dev, uint4* __restrict__ host, uint32_t g16,
+                                                   uint32_t reply16, uint32_t n_max, uint32_t with_reply) {
+  const uint32_t c = with_reply ? min(*reinterpret_cast<const uint32_t*>(dev + reply16), n_max) : 0u;
+  const uint32_t r16 = with_reply ? 1u + (c * 8u + 15u) / 16u : 0u;
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < g16 + r16; k += gridDim.x * 256) {
+    const uint32_t j = k < g16 ? k : reply16 + (k - g16);
+    host[j] = dev[j];
+  }
+}
+
 // Harness `setup` (state_machine.zig:2545-2561).
 __global__ void k_setup(Dev d, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dpo, tb_uint128_t cp, tb_uint128_t cpo,
                         int* found) {

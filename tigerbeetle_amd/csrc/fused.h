@@ -171,6 +171,15 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
   o->simple = simple;
 }
 
+// A per-window count kept as [63:32] epoch | [31:0] count and never reset: the block's atomicMax moves a
+// stale tag to this epoch with count 0 (a no-op once it is there), then its atomicAdd returns the
+// count before it. Two atomics per block, where a compare-and-swap loop measured quadratic in the
+// blocks contending for it (16 ms per 1M-event window with a count in every block).
+__device__ __forceinline__ uint32_t epoch_count_add(unsigned long long* word, uint32_t epoch, uint32_t n) {
+  (void)atomicMax(word, (unsigned long long)epoch << 32);
+  return (uint32_t)atomicAdd(word, (unsigned long long)n);
+}
+
 // Scratch of the fused pass (per 256-event block; per 64-event wave).
 struct FuScratch {
   uint32_t* cnt;            // per block: failed events
@@ -181,7 +190,20 @@ struct FuScratch {
   unsigned long long* pend; // per wave: ok pending creates
   unsigned long long* pto;  // per wave: ok pending creates with a timeout the expiry scan can see
   unsigned long long* pnmin;  // per block: smallest expiry of its ok creates with a timeout (~0: none)
+  uint32_t* pbase;          // per block: its first live expiry entry within its slot (fu_slot_base)
+  unsigned long long* slots;  // FU_SLOTS failure counts, then FU_SLOTS expiry-entry counts (epoch_count_add)
 };
+
+// Window-wide counts spread over FU_SLOTS words (block k adds to slot k % FU_SLOTS): same-address
+// atomics serialize at the L2 (~30 ns each with a return; one per block of a 1M-event window cost
+// 240 us), one slot per 64 blocks does not. Readers sum the slots with one wave.
+#define FU_SLOTS 64
+// Lane j < FU_SLOTS of the calling wave: slot j's count for this epoch (0 when stale).
+__device__ __forceinline__ uint32_t fu_slot_count(const unsigned long long* slots, uint32_t epoch) {
+  const uint32_t j = threadIdx.x & 63;
+  const unsigned long long v = slots[j];
+  return (uint32_t)(v >> 32) == epoch ? (uint32_t)v : 0u;
+}
 
 // The balance fields a create adds to: posted, or pending for a pending transfer (:1555-1566).
 __device__ __forceinline__ unsigned long long* fu_dr_field(const Dev& d, const FuEv& fe) {
@@ -219,17 +241,38 @@ __device__ __forceinline__ void fu_store_records(Dev d, const uint4* src, bool o
 // at or beyond the store's end) and, when its events are simple, the balance adds.
 __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
                                                    WinDesc w, uint32_t epoch, uint32_t fo_only, uint32_t* fmark,
-                                                   uint32_t pn_skip) {
+                                                   uint32_t pn_skip, uint4* __restrict__ ev_copy) {
   __shared__ uint4 stage[FU_T * 4];  // half of each inserted record per round (16 KiB)
   __shared__ uint32_t lds[FU_T / 64];
   __shared__ unsigned long long ldsu[FU_T / 64];
   __shared__ u128 ldsm[FU_T / 64];
   __shared__ uint32_t ldsn[FU_T / 64];
   __shared__ unsigned long long ldsp[FU_T / 64];
+  __shared__ uint32_t ldsx[FU_T / 64];
   Globals* g = d.g;
-  if (WIN_REJECTED(g)) return;
+  const bool rejected = WIN_REJECTED(g);
   const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (g->sp_skip) {  // backed off: the general path decides this window
+  // Another block may flag the window at any time, so waves of this block can read fu_abort
+  // differently: each wave reads it once (wave-uniform), and the block applies its adds only if NO
+  // wave saw it set (folded into the block vote below), so every wave and fs.applied[k] agree on
+  // whether this block applies (k_fu_final undoes exactly those).
+  const bool skip = !rejected && g->sp_skip != 0;
+  const bool aborted = rejected || skip || __builtin_amdgcn_readfirstlane(__hip_atomic_load(&g->fu_abort, __ATOMIC_RELAXED,
+                                                                                __HIP_MEMORY_SCOPE_AGENT) == epoch
+                                                                  ? 1
+                                                                  : 0) != 0;
+  // ev_copy (the synchronous path): `ev` is the request in pinned host memory, read once over the link
+  // by this pass, which stores it to ev_copy in HBM as it goes (every later kernel and a replay read
+  // that), whatever the window's fate, instead of a separate copy launch ahead of it. A wave that does
+  // not decide copies its 64 records here.
+  if (ev_copy && aborted) {
+    const uint32_t i0 = k * FU_T + wave * 64;
+    const uint32_t n16 = i0 < w.E ? min(64u, w.E - i0) * 8u : 0u;
+    const uint4* src = reinterpret_cast<const uint4*>(ev + i0);
+    for (uint32_t q = lane; q < n16; q += 64) ev_copy[(size_t)i0 * 8 + q] = src[q];
+  }
+  if (rejected) return;
+  if (skip) {  // backed off: the general path decides this window
     if (k == 0 && threadIdx.x == 0) {
       g->sp_done = 0;
       // a fused-only window has no general path behind it (a non-fused-only window outside the class
@@ -259,16 +302,11 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
     // what k_fu_final reads while its last block updates the store counts
     g->fu_epoch = epoch;
     g->fu_base = base;
+    g->fu_exp_base = g->exp_count;  // (unchanged until k_fu_final's last block)
     // the window may extend the sorted prefix (first id above every stored id; its ids must rise
     // too: Globals::fu_nonmono, k_fu_final)
     g->fu_prefix = (P == base && U(ev[0].id) > x_id_max) ? 1u : 0u;
   }
-  // Another block may flag the window at any time, so waves of this block can read fu_abort
-  // differently: each wave reads it once (wave-uniform), and the block applies its adds only if NO
-  // wave saw it set (folded into the block vote below), so every wave and fs.applied[k] agree on
-  // whether this block applies (k_fu_final undoes exactly those).
-  const bool aborted = __builtin_amdgcn_readfirstlane(
-                           __hip_atomic_load(&g->fu_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch ? 1 : 0) != 0;
 
   tb_transfer_t t;
   FuEv fe;
@@ -293,7 +331,11 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
 #pragma unroll
       for (int c = 0; c < 4; c++) {
         const uint32_t idx = c * 64 + lane, r = idx >> 2, q = idx & 3;
-        if (r < nrec) ws[r * 4 + (q ^ ((r >> 2) & 3))] = ld_stream(src + r * 8 + half * 4 + q);
+        if (r < nrec) {
+          const uint4 v = ld_stream(src + r * 8 + half * 4 + q);
+          ws[r * 4 + (q ^ ((r >> 2) & 3))] = v;
+          if (ev_copy) ev_copy[(size_t)(i0 + r) * 8 + half * 4 + q] = v;
+        }
       }
       wave_sync();
 #pragma unroll
@@ -367,10 +409,11 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
     ldsm[wave] = wmax;
     ldsn[wave] = wnm ? 1u : 0u;
     ldsp[wave] = pmin;
+    ldsx[wave] = (uint32_t)__popcll(ptom);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t nbad = 0, nm = 0;
+    uint32_t nbad = 0, nm = 0, nexp = 0;
     unsigned long long bsum = 0, bpmin = ~0ull;
     u128 bmax = 0;
 #pragma unroll
@@ -380,25 +423,21 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
       bmax = umax128(bmax, ldsm[q]);
       nm |= ldsn[q];
       bpmin = ldsp[q] < bpmin ? ldsp[q] : bpmin;
+      nexp += ldsx[q];
     }
     fs.cnt[k] = nbad;
+    if (nexp) {
+      // this block's live expiry entries: one reservation per block (k_fu_final writes them; per-wave
+      // appends there serialized ~16K same-address atomics per 1M-event window of 1 % pending creates)
+      fs.pbase[k] = epoch_count_add(fs.slots + FU_SLOTS + k % FU_SLOTS, epoch, nexp);
+    }
     fs.pnmin[k] = bpmin;
     // (claim mode) this block's ids do not rise: the window is hashed, and the next one claims too
     if (nm) __hip_atomic_store(&g->fu_nonmono, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     fs.pay[k] = bsum;
     fs.idmax[k] = bmax;
-    if (nbad) {
-      // the window's failure count, tagged with its epoch (no reset between windows)
-      unsigned long long* acc = reinterpret_cast<unsigned long long*>(&g->fu_bad);
-      unsigned long long old = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (;;) {
-        const unsigned long long nv = ((unsigned long long)epoch << 32) |
-                                      (((uint32_t)(old >> 32) == epoch ? (uint32_t)old : 0u) + nbad);
-        const unsigned long long seen = atomicCAS(acc, old, nv);
-        if (seen == old) break;
-        old = seen;
-      }
-    }
+    // the window's failure count, tagged with its epoch (no reset between windows)
+    if (nbad) (void)epoch_count_add(fs.slots + k % FU_SLOTS, epoch, nbad);
   }
 }
 
@@ -448,8 +487,13 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
   const uint64_t base = g->fu_base;
   const bool mono = g->fu_nonmono != epoch;
   const bool prefix_win = g->fu_prefix != 0 && mono;
-  const unsigned long long bw = g->fu_bad;
-  const uint32_t total_bad = (uint32_t)(bw >> 32) == epoch ? (uint32_t)bw : 0u;
+  __shared__ uint32_t tb_lds;
+  if (threadIdx.x < 64) {  // the window's failures: the slots summed by the first wave
+    const uint32_t t = wave_sum(fu_slot_count(fs.slots, epoch));
+    if (threadIdx.x == 0) tb_lds = t;
+  }
+  __syncthreads();
+  const uint32_t total_bad = tb_lds;
   if (!total_bad && prefix_win && k != gridDim.x - 1 && fs.pnmin[k] == ~0ull) {
     // nothing moves, nothing to index, no expiry entry: only a block where a batch starts has a reply
     // base to write
@@ -500,23 +544,24 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
     fu_store_records(d, rec, ok, okm, base + r0, stage + wave * 256);
   }
   if (ok && !prefix_win) x_insert(d.x_tab, d.x_mask, ev[i].id, (uint32_t)(base + rins));
-  {
-    // live expires_at entries of the window's pending creates with a timeout (one atomic per wave)
-    const unsigned long long m = __ballot(pto);
-    if (m) {
-      const int leader = __builtin_ctzll(m);
-      unsigned long long q = 0;
-      if ((int)lane == leader)
-        q = atomicAdd(reinterpret_cast<unsigned long long*>(&g->exp_count), (unsigned long long)__popcll(m));
-      q = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(q >> 32), leader) << 32) |
-          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q, leader);
-      if (pto) {
-        ExpEntry x;
-        x.expires_at = win_ts(w, win_batch(w, i), i) + (uint64_t)ev[i].timeout * TB_NS_PER_S;
-        x.slot = (uint32_t)(base + rins);
-        x.pad = 0;
-        d.exp[*d.exp_cur][q + (unsigned long long)__popcll(m & ((1ull << lane) - 1))] = x;
-      }
+  if (__syncthreads_or(pto)) {
+    // live expires_at entries of the window's pending creates with a timeout, in event order, at this
+    // block's reservation (k_ct_fused): after the entries of the slots before its own
+    __shared__ uint32_t xbase_lds;
+    if (threadIdx.x < 64) {
+      const uint32_t c = fu_slot_count(fs.slots + FU_SLOTS, epoch);
+      const uint32_t before = wave_sum(threadIdx.x < k % FU_SLOTS ? c : 0u);
+      if (threadIdx.x == 0) xbase_lds = before;
+    }
+    __syncthreads();
+    uint32_t nx;
+    const uint32_t rx = block_excl<FU_T / 64>(pto ? 1u : 0u, lds, &nx);
+    if (pto) {
+      ExpEntry x;
+      x.expires_at = win_ts(w, win_batch(w, i), i) + (uint64_t)ev[i].timeout * TB_NS_PER_S;
+      x.slot = (uint32_t)(base + rins);
+      x.pad = 0;
+      d.exp[*d.exp_cur][g->fu_exp_base + xbase_lds + fs.pbase[k] + rx] = x;
     }
   }
   if (k == gridDim.x - 1) {
@@ -540,7 +585,13 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
       redm[wave] = mx;
       redp[wave] = pn;
     }
+    __shared__ uint32_t xtot_lds;
+    if (threadIdx.x < 64) {  // the window's live expiry entries over all slots
+      const uint32_t t = wave_sum(fu_slot_count(fs.slots + FU_SLOTS, epoch));
+      if (threadIdx.x == 0) xtot_lds = t;
+    }
     __syncthreads();
+    const uint32_t xtot = xtot_lds;
     if (threadIdx.x == 0) {
       for (uint32_t q = 1; q < FU_T / 64; q++) {
         sum += red[q];
@@ -548,6 +599,7 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
         pn = redp[q] < pn ? redp[q] : pn;
       }
       if (pn < g->pulse_next) g->pulse_next = pn;  // :1576-1581
+      g->exp_count = g->fu_exp_base + xtot;
       const uint32_t total_ins = E - total_bad;
       for (int32_t bb = (int32_t)w.nb; bb >= 0 && w.off[bb] == E; bb--) o.batch_base[bb] = total_bad;
       if (o.out_count) *o.out_count = total_bad;

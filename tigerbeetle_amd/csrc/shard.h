@@ -10,7 +10,7 @@
 //                 when the window's ids are not known to rise, and compares it with a stored transfer
 //                 (`exists`, :1506-1507); the debit / credit owners resolve their account (state
 //                 against the event's ledger, limit flags) and keep its slot. Each owner writes its part
-//                 of the event's 2 B of facts; the last block folds this shard's verdicts.
+//                 of the event's 2 B of facts; each block ORs its verdicts into the trailer itself.
 //   (caller)      exchange 1: byte-wise sum all-reduce of the facts (RCCL over xGMI). Every bit has
 //                 exactly one writer, so the sum is the union.
 //   k_sh_decide   every event on every shard, from the facts alone: account lookups (:1496-1497),
@@ -34,14 +34,21 @@
 
 // Exchange bytes of a window of E events over G shards (summed byte-wise over the shards: every bit
 // has exactly one writer, so the byte sum is the union with no carries; one uint8 all-reduce):
-//   [0, 16)         trailer: word 0 this shard's verdict bytes (k_sh_scan; ZW_* below), the rest zero
-//   [16, 16+E)      the id owner's byte: 1 + the code, static / linked bits (ZW_*)
+//   [0, 16)         trailer: word `par` (the window's parity, 0 / 1) this shard's verdict bytes (k_sh_scan;
+//                   ZW_* below); the other word zeroed for the next window by this one's scan; words 2-3 zero
+//   [16, M)         fixed-size counters, zeroed for the next window by k_sh_apply (each word has one writer
+//                   shard, so the byte sum keeps it whole):
+//                     G u64: shard g's room in its store (x_max - x_count or acc_max - acc_count)
+//                     G x SH_OWN_SLOTS u32: shard g's owned ids reaching the exists check, by scan block
+//                       k in slot k % SH_OWN_SLOTS (no-return adds: no same-address serialization)
+//                     G x SH_MIS_SLOTS u64 ledger-mismatch slots, shard g's at [g * SH_MIS_SLOTS, ...):
+//                       valid << 63 | side << 52 | event << 32 | the account's ledger
+//                   M = 16 + 8 G + 4 G SH_OWN_SLOTS + 8 G SH_MIS_SLOTS
+//   [M, M+E)        the id owner's byte: 1 + the code, static / linked bits (ZW_*)
 //   create_transfers:
-//   [16+E, 16+2E)   the account sides' states (SH_ACC_*): bits 0-1 the debit account, 2-3 the credit
+//   [M+E, M+2E)     the account sides' states (SH_ACC_*): bits 0-1 the debit account, 2-3 the credit
 //                   account, each by its owner against the event's ledger; bits 4 / 5 the limit or
 //                   history flag of the debit / credit account
-//   [16+2E, ...)    G x SH_MIS_SLOTS u64 ledger-mismatch slots, shard g's at [g * SH_MIS_SLOTS, ...):
-//                   valid << 63 | side << 52 | event << 32 | the account's ledger
 // A side's ledger is needed only when both accounts mismatch the event's ledger (then whether they
 // match each other decides between accounts_must_have_the_same_ledger and
 // transfer_must_have_the_same_ledger_as_accounts, :1503-1504), so the 8 B of ledgers per event of the
@@ -49,25 +56,36 @@
 enum : uint32_t { SH_ACC_OK = 1, SH_ACC_MISSING = 2, SH_ACC_MISMATCH = 3 };
 #define SH_MIS_SLOTS 4096u  // per shard; more mismatches in one window: outside the class (trailer 0)
 
+#define SH_OWN_SLOTS 64u
 struct XchView {
   uint32_t* trailer;
+  unsigned long long* room;  // G
+  uint32_t* own;             // G x SH_OWN_SLOTS
+  unsigned long long* mis;   // G x SH_MIS_SLOTS (transfers only use them)
   uint8_t* zw;
   uint8_t* acc;              // transfers only
-  unsigned long long* mis;   // transfers only: G x SH_MIS_SLOTS
   uint32_t G;
+  uint32_t par;              // the window's trailer word
 };
-__host__ __device__ inline uint64_t xch_mis_off(uint32_t E) { return (16 + 2ull * E + 7) & ~7ull; }
-__host__ __device__ inline uint64_t xch_bytes(bool xfer, uint32_t E, uint32_t G) {
-  return xfer ? xch_mis_off(E) + 8ull * G * SH_MIS_SLOTS : 16 + (uint64_t)E;
+// the fixed-size counters after the trailer: rooms, owned-id slots, mismatch slots (k_sh_apply zeroes them)
+__host__ __device__ inline uint64_t xch_counters_words(uint32_t G) {  // (in u32 words)
+  return 2ull * G + (uint64_t)G * SH_OWN_SLOTS + 2ull * G * SH_MIS_SLOTS;
 }
-__host__ __device__ inline XchView xch_view(void* base, uint32_t E, bool xfer, uint32_t G) {
+__host__ __device__ inline uint64_t xch_facts_off(uint32_t G) { return 16 + 4 * xch_counters_words(G); }
+__host__ __device__ inline uint64_t xch_bytes(bool xfer, uint32_t E, uint32_t G) {
+  return xch_facts_off(G) + (xfer ? 2ull : 1ull) * E;
+}
+__host__ __device__ inline XchView xch_view(void* base, uint32_t E, bool xfer, uint32_t G, uint32_t par) {
   uint8_t* p = reinterpret_cast<uint8_t*>(base);
   XchView v;
   v.trailer = reinterpret_cast<uint32_t*>(p);
-  v.zw = p + 16;
-  v.acc = xfer ? p + 16 + E : nullptr;
-  v.mis = xfer ? reinterpret_cast<unsigned long long*>(p + xch_mis_off(E)) : nullptr;
+  v.room = reinterpret_cast<unsigned long long*>(p + 16);
+  v.own = reinterpret_cast<uint32_t*>(p + 16 + 8ull * G);
+  v.mis = reinterpret_cast<unsigned long long*>(p + 16 + 8ull * G + 4ull * G * SH_OWN_SLOTS);
+  v.zw = p + xch_facts_off(G);
+  v.acc = xfer ? v.zw + E : nullptr;
   v.G = G;
+  v.par = par;
   return v;
 }
 // A side's ledger from the mismatch slots (both sides mismatched; never expected to be missing).
@@ -146,7 +164,7 @@ __device__ inline void sh_window_reset(Globals* g, bool xfer, uint64_t count, bo
   g->batch_huge = 0;
 }
 
-// Scan-block partials (Scratch::blk_aux): bit 0 huge amount, bit 1 in-window duplicate id (outside the
+// Scan-block partials (k_sh_scan's LDS word, then Globals::sh_flags): bit 0 huge amount, bit 1 in-window duplicate id (outside the
 // class), bit 2 ids not strictly increasing (or >= 2^64), bit 3 the window's first id is above every
 // stored id, bit 4 an event outside the class (SHX_UNSUP), owned ids reaching the exists check << 5.
 enum : uint32_t { SHX_HUGE = 1, SHX_DUP = 2, SHX_NONMONO = 4, SHX_FRESH = 8, SHX_OWN_SHIFT = 5 };
@@ -222,7 +240,7 @@ static_assert(TB_CT_EXCEEDS_DEBITS + 1 <= (int)ZW_CODE && TB_CA_EXISTS + 1 <= (i
 enum : uint32_t { SHX_UNSUP = 16 };
 #define SH_SCAN_T 256  // k_sh_scan's block: small blocks keep more of its latency-bound waves resident
 
-__device__ inline bool sh_verdict(const XchView& x) { return x.trailer[0] != 0; }
+__device__ inline bool sh_verdict(const XchView& x) { return x.trailer[x.par] != 0; }
 
 // ------------------------------------------------------------------------------------------------
 // k_sh_scan (before exchange 1): one pass over the window, one event per thread, every shard. Each
@@ -230,10 +248,13 @@ __device__ inline bool sh_verdict(const XchView& x) { return x.trailer[0] != 0; 
 // validates the event (state_machine.zig:1424-1439, 1465-1489), claims its id when the window's ids
 // are not known to rise (in-window duplicates through the window key map) and compares it with a
 // stored transfer (`exists`, :1506-1507); the debit / credit owners resolve their account (state
-// against the event's ledger, limit and history flags) and keep its slot for k_sh_apply. Then
-// k_sh_fold (one block) folds the blocks' partials into this shard's verdicts (exchange 1's trailer)
-// and the window's overflow / prefix state. (A last-block-done fold inside the scan measured ~2x
-// slower: its agent-scope fence per block writes the XCD's L2 back.)
+// against the event's ledger, limit and history flags) and keep its slot for k_sh_apply. Each block
+// ORs its rare verdicts into the trailer, adds its owned-id count to a slot of the exchange (every
+// shard checks every shard's room after the exchange) and writes its partials (Scratch::blk_aux,
+// blk_amt), which k_sh_decide's first block folds after the exchange: no fold launch, no grid-wide
+// wait, no same-address atomic per block. (A last-block-done fold inside the scan measured ~2x
+// slower: its agent-scope fence per block writes the XCD's L2 back; a one-block fold launch cost
+// ~8 us + a launch gap per window; per-block returning atomics on Globals words ~50 us per 1M events.)
 // ------------------------------------------------------------------------------------------------
 template <bool XFER>
 __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes,
@@ -250,10 +271,16 @@ __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const u
       s.cnt_ins[i / SEG] = 0;
     }
   }
-  if (i == 0) check_window(w, g);
-  if (XFER)  // the other shards' mismatch slots are zero in this shard's copy (its own: k_sh_fold)
-    for (uint32_t k = i; k < G * SH_MIS_SLOTS; k += gridDim.x * SH_SCAN_T)
-      if (k / SH_MIS_SLOTS != me) xch.mis[k] = 0;
+  if (i == 0) {
+    check_window(w, g);
+    g->sh_unsup = 0;              // (k_sh_decide: a committed event reading a balance)
+    xch.trailer[xch.par ^ 1] = 0;  // the next window's verdict word (its last reader was k_sh_apply)
+    xch.room[me] = XFER ? d.x_max - g->x_count : d.acc_max - g->acc_count;
+    // the overflow bound (a verdict, so every shard agrees): the window's owned amounts are each below
+    // 2^64 (larger ones: SHX_HUGE) and at most E of them, so ovf_bound + E x 2^64 bounds the sum
+    if (XFER && g->ovf_bound > MAX128 - ((u128)E << 64)) atomicOr(&xch.trailer[xch.par], 1u << 16);
+  }
+  // (the mismatch slots are zero: the previous window's k_sh_apply cleared them)
   __syncthreads();
   // the previous fast-path window's ids did not all rise: claims find in-window duplicates
   const bool claim = !XFER || g->mono_prev == 0;
@@ -329,7 +356,7 @@ __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const u
             const uint32_t k2 = atomicAdd(&g->sh_mis, 1u);
             if (k2 < SH_MIS_SLOTS)
               xch.mis[me * SH_MIS_SLOTS + k2] = (1ull << 63) | ((unsigned long long)side << 52) |
-                                                ((unsigned long long)i << 32) | e.ledger;
+                                                ((unsigned long long)i << 32) | e.ledger;  // (k_sh_decide resets sh_mis)
             else
               atomicOr(&aux, (uint32_t)SHX_DUP);  // (verdict 0: outside the class)
           }
@@ -362,74 +389,19 @@ __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const u
     u128 tot = 0;
 #pragma unroll
     for (int w2 = 0; w2 < SH_SCAN_T / 64; w2++) tot += red[w2];
+    const uint32_t bits = aux & 31u, own = aux >> SHX_OWN_SHIFT;
     s.blk_amt[blockIdx.x] = tot;
-    s.blk_aux[blockIdx.x] = aux;
+    s.blk_aux[blockIdx.x] = bits;
+    // this block's verdicts (bytes of this shard's trailer word: [0] duplicate / unchecked
+    // non-rising ids / mismatch slots full, [2] overflow bound, [3] outside the class; [1] capacity
+    // is decided from the owned-id slots after the exchange)
+    const bool claim = !XFER || g->mono_prev == 0;  // (k_sh_decide updates it after this launch)
+    uint32_t v = ((bits & SHX_DUP) || (XFER && (bits & SHX_NONMONO) && !claim)) ? 1u : 0u;
+    if (bits & SHX_HUGE) v |= 1u << 16;
+    if (bits & SHX_UNSUP) v |= 1u << 24;
+    if (v) atomicOr(&xch.trailer[xch.par], v);
+    if (own) (void)atomicAdd(&xch.own[me * SH_OWN_SLOTS + blockIdx.x % SH_OWN_SLOTS], own);
   }
-}
-
-// After k_sh_scan, one block: this shard's verdicts into exchange 1's trailer, the window's overflow /
-// prefix / claim state into Globals, this shard's unused mismatch slots zeroed.
-template <bool XFER>
-__global__ void __launch_bounds__(SEG) k_sh_fold(Dev d, Scratch s, uint32_t nblk, XchView xch, uint32_t me) {
-  __shared__ u128 red[SEG / 64];
-  __shared__ uint32_t aux;
-  __shared__ unsigned long long own_s;
-  Globals* g = d.g;
-  const bool claim = !XFER || g->mono_prev == 0;  // (what k_sh_scan read)
-  if (threadIdx.x == 0) {
-    aux = 0;
-    own_s = 0;
-  }
-  __syncthreads();
-  u128 vt = 0;
-  uint32_t ab = 0;
-  unsigned long long own = 0;
-  for (uint32_t j = threadIdx.x; j < nblk; j += SEG) {
-    const uint32_t x = s.blk_aux[j];
-    ab |= x & 31u;
-    own += x >> SHX_OWN_SHIFT;
-    if (XFER) vt += s.blk_amt[j];
-  }
-  if (ab) atomicOr(&aux, ab);
-  if (own) atomicAdd(&own_s, own);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t lo = __shfl_xor((unsigned long long)(uint64_t)vt, o, 64);
-    const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(vt >> 64), o, 64);
-    vt += ((u128)hi << 64) | lo;
-  }
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = vt;
-  // this shard's mismatch slots beyond the ones it used are zero in its copy
-  if (XFER) {
-    const uint32_t used = min(g->sh_mis, SH_MIS_SLOTS);
-    for (uint32_t k = used + threadIdx.x; k < SH_MIS_SLOTS; k += SEG) xch.mis[me * SH_MIS_SLOTS + k] = 0;
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  u128 tot = 0;
-  for (int w2 = 0; w2 < SEG / 64; w2++) tot += red[w2];
-  const uint32_t bits = aux;
-  uint32_t v0 = (bits & SHX_DUP) ? 1u : 0u, v1 = 0, v2 = 0;
-  const uint32_t v3 = (bits & SHX_UNSUP) ? 1u : 0u;
-  if (XFER) {
-    if ((bits & SHX_NONMONO) && !claim) v0 = 1;  // duplicates were not looked for
-    g->batch_amount_sum += tot;
-    if (bits & SHX_HUGE) g->batch_huge = 1;
-    v1 = g->x_count + own_s > d.x_max ? 1u : 0u;
-    v2 = window_ovf_mode(g) ? 1u : 0u;
-    // every owned balance field stays below 2^64 this window: k_sh_apply's adds need no carry
-    const u128 top = g->ovf_bound + g->batch_amount_sum;
-    g->small_win = (!g->batch_huge && top >= g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1u : 0u;
-    const bool prefix = !(bits & SHX_NONMONO) && (bits & SHX_FRESH) && g->x_sorted == g->x_count;
-    g->win_flags = prefix ? 2u : 0u;
-    g->mono_prev = (bits & SHX_NONMONO) ? 0u : 1u;  // the next window's claim mode (the same on every shard)
-    g->sh_mis = 0;
-  } else {
-    v1 = g->acc_count + own_s > d.acc_max ? 1u : 0u;
-  }
-  g->sh_unsup = 0;  // (k_sh_decide: a committed event reading a balance)
-  xch.trailer[0] = v0 | (v1 << 8) | (v2 << 16) | (v3 << 24);
-  xch.trailer[1] = xch.trailer[2] = xch.trailer[3] = 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -463,8 +435,55 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
   __shared__ uint32_t nbad, nins;
   __shared__ u128 ldsm[SEG / 64];
   Globals* g = d.g;
+  if (blockIdx.x == 0) {
+    // k_sh_scan's partials folded (read by k_sh_apply and the next window; nothing else here reads
+    // them), whatever the verdict: its blocks' flags and amounts, and every shard's owned inserts
+    // against its room (the same capacity verdict on every shard)
+    __shared__ uint32_t f_bits, f_cap;
+    __shared__ u128 f_red[SEG / 64];
+    if (threadIdx.x == 0) f_bits = f_cap = 0;
+    __syncthreads();
+    const uint32_t nblk = (w.E + SH_SCAN_T - 1) / SH_SCAN_T;
+    uint32_t fb = 0;
+    u128 fa = 0;
+    for (uint32_t j = threadIdx.x; j < nblk; j += SEG) {
+      fb |= s.blk_aux[j];
+      if (XFER) fa += s.blk_amt[j];
+    }
+    if (fb) atomicOr(&f_bits, fb);
+    if (threadIdx.x < xch.G) {
+      uint64_t tot = 0;
+      for (uint32_t q = 0; q < SH_OWN_SLOTS; q++) tot += xch.own[threadIdx.x * SH_OWN_SLOTS + q];
+      if (tot > xch.room[threadIdx.x]) atomicOr(&f_cap, 1u);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t lo = __shfl_xor((unsigned long long)(uint64_t)fa, o, 64);
+      const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(fa >> 64), o, 64);
+      fa += ((u128)hi << 64) | lo;
+    }
+    if ((threadIdx.x & 63) == 0) f_red[threadIdx.x >> 6] = fa;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t bits = f_bits;
+      g->sh_cap_bad = f_cap;
+      if (XFER) {
+        u128 amt = 0;
+        for (int q = 0; q < SEG / 64; q++) amt += f_red[q];
+        g->batch_amount_sum += amt;
+        if (bits & SHX_HUGE) g->batch_huge = 1;
+        // every owned balance field stays below 2^64 this window: k_sh_apply's adds need no carry
+        const u128 top = g->ovf_bound + g->batch_amount_sum;
+        g->small_win = (!g->batch_huge && top >= g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1u : 0u;
+        const bool prefix = !(bits & SHX_NONMONO) && (bits & SHX_FRESH) && g->x_sorted == g->x_count;
+        g->win_flags = prefix ? 2u : 0u;
+        g->mono_prev = (bits & SHX_NONMONO) ? 0u : 1u;  // the next window's claim mode (the same on every shard)
+        g->sh_mis = 0;
+      }
+      g->base = XFER ? g->x_count : g->acc_count;  // k_sh_apply's insert base
+    }
+  }
   if (sh_verdict(xch)) return;  // outside the class: k_sh_apply reports it
-  if (blockIdx.x == 0 && threadIdx.x == 0) g->base = XFER ? g->x_count : g->acc_count;  // k_sh_apply's insert base
   if (threadIdx.x == 0) nbad = nins = 0;
   __syncthreads();
   const uint32_t i = blockIdx.x * SEG + threadIdx.x, seg = blockIdx.x;
@@ -534,7 +553,9 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
 // and indexes it. The last block folds the inserted ids' exact maximum and closes the window. A window outside the class (exchange 1's verdict, or a committed event reading a balance)
 // changes nothing on any shard: window_error bit 1 (TBG_E_UNSUPPORTED at tbg_sync).
 // ------------------------------------------------------------------------------------------------
-__device__ inline bool sh_abort(const XchView& x, const Globals* g) { return sh_verdict(x) || g->sh_unsup != 0; }
+__device__ inline bool sh_abort(const XchView& x, const Globals* g) {
+  return sh_verdict(x) || g->sh_unsup != 0 || g->sh_cap_bad != 0;
+}
 
 // STAGE (one shard: every event is owned, the inserts are dense): a wave's inserted records are
 // compacted in LDS and stored as one contiguous run (as in k_final); with several shards the inserts
@@ -548,6 +569,10 @@ __global__ void __launch_bounds__(SEG) __attribute__((amdgpu_waves_per_eu(STAGE 
   __shared__ u128 ldsm[SEG / 64];
   __shared__ uint4 stage[XFER && STAGE ? SEG * 8 : 1];
   Globals* g = d.g;
+  // the counters zeroed for the next window (k_sh_decide was their last reader)
+  const uint32_t nw = (uint32_t)xch_counters_words(xch.G);
+  uint32_t* cw = reinterpret_cast<uint32_t*>(xch.room);
+  for (uint32_t k = blockIdx.x * SEG + threadIdx.x; k < nw; k += gridDim.x * SEG) cw[k] = 0;
   if (sh_abort(xch, g)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       atomicOr(&g->window_error, 2u);

@@ -15,8 +15,22 @@ struct WinDesc {
   uint32_t off[MAXB + 1];  // event offset of each batch; off[nb] = E
   uint32_t xwin;           // pulses inside the window are modelled (xwin.h): it spans >= 1 s
   uint32_t log;            // TBG_WINDOW_LOG: batches from a replica's log, no pulse between them
+  uint32_t bsz;            // nonzero: every batch but the last has bsz events, the last at most bsz
   uint64_t T[MAXB];        // commit timestamp of each batch
 };
+
+// WinDesc::bsz from the offsets (host): the common shape of a window of full batches, so that an
+// event's batch is a division rather than a binary search over off[] (eight dependent loads from the
+// kernel arguments per event).
+inline void win_set_bsz(WinDesc* w) {
+  w->bsz = 0;
+  const uint32_t n0 = w->off[1] - w->off[0];
+  if (n0 == 0) return;
+  for (uint32_t b = 1; b + 1 < w->nb; b++)
+    if (w->off[b + 1] - w->off[b] != n0) return;
+  if (w->E - w->off[w->nb - 1] > n0) return;
+  w->bsz = n0;
+}
 
 // The first batch of the window whose pulse check (T_b >= expires_at) finds an entry due: the pulse
 // that expires it (xwin.h; MAXB = window's nb when none).
@@ -30,6 +44,10 @@ __device__ inline uint32_t xw_due(const WinDesc& w, uint64_t expires_at) {
 }
 
 __device__ inline uint32_t win_batch(const WinDesc& w, uint32_t i) {
+  if (w.bsz) {
+    const uint32_t b = i / w.bsz;
+    return b < w.nb ? b : w.nb - 1;
+  }
   uint32_t lo = 0, hi = w.nb - 1;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) >> 1;

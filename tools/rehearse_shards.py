@@ -142,6 +142,9 @@ def general(a):
     one.close()
 
 
+SLEEP_CYCLES = 400_000  # ~0.2 ms of GPU clock ahead of each timed step
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--shards", type=int, default=8)
@@ -185,6 +188,8 @@ def main():
         for r, s in enumerate(shards):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             with torch.cuda.stream(s.stream):
+                # keep the GPU busy while the host submits, so e0..e1 is device time, not launch latency
+                torch.cuda._sleep(SLEEP_CYCLES)
                 e0.record()
                 outs.append(fn(r, s))
                 e1.record()
@@ -241,7 +246,7 @@ def main():
                                 "decide_apply_mean": round(float(t[:, :, 1].mean()), 4),
                                 "max_shard_mean": round(float(per_shard.max(axis=1).mean()), 4)},
         "estimated_rate_excl_collective": round(events / crit, 1),
-        "exchange_bytes_per_window": 16 + 2 * win * BATCH + 8 * G * 4096,
+        "exchange_bytes_per_window": int(L.tbg_shard_exchange_bytes(int(Operation.create_transfers), win * BATCH, G)),
         "stats_shard0": shards[0].stats(),
     }
     print(json.dumps(out), flush=True)

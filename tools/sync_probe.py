@@ -20,6 +20,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--batches", type=int, default=64)
     p.add_argument("--accounts", type=int, default=100_000)
+    p.add_argument("--no-copy-probe", action="store_true", help="end after the raw ABI loop (device timelines)")
     a = p.parse_args()
     import torch
 
@@ -90,6 +91,9 @@ def main():
     out["raw_abi"] = {"us_per_batch": round((time.perf_counter() - t0) / k * 1e6, 1),
                       "pulse_us": round(tp / k * 1e6, 1), "prefetch_us": round(tf / k * 1e6, 1),
                       "commit_us": round(tc / k * 1e6, 1)}
+    if a.no_copy_probe:
+        print(json.dumps(out), flush=True)
+        return
     # the bare copy: one 1 MiB H2D from pinned memory, synchronized
     dst = torch.empty(BATCH * 128, dtype=torch.uint8, device="cuda")
     src = torch.from_numpy(bodies[0])
