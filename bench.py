@@ -72,7 +72,7 @@ PHASE_KERNELS = {
     "cpw": ["k_cc_walk<true>", "k_cc_init", "k_cc_link", "k_cc_keys", "onesweep sort", "k_cc_segs"],
     "classify": ["k_classify<true>"], "wlist": ["k_wlist"], "walk": ["k_walk<true>", "k_wfold"],
     "pulse": ["k_pulse", "k_xwin_rb", "k_xwin_minlive", "k_xwin_replay", "k_xwin_expire"],
-    "fused": ["k_ct_fused"],  # k_fu_final (replies, ~12 us per 1M) runs outside the timed phase
+    "fused": ["k_ct_fused<false>"],  # k_fu_final (replies, ~12 us per 1M) runs outside the timed phase
 }
 # the walkers (cpw, walk) run the reference loop for the events they decide: event 128, balance
 # pairs 2 x 32, record 128 per walked event
@@ -103,20 +103,35 @@ def warm_phases(sm, nph):
     return per_phase, dom
 
 
+def pmc_tag(args):
+    """The name of this bench line's PMC summary: the config, then the options that change the
+    kernels' traffic (the id order, the change log, the pending share), e.g. cfg2_random."""
+    tag = args.config
+    if args.id_order != "sequential":
+        tag += "_" + args.id_order
+    if args.change_log:
+        tag += "_changelog"
+    if args.pending_every:
+        tag += "_pending%d" % args.pending_every
+    return tag
+
+
 def pmc_traffic(config, kernel, events_per_launch):
-    """Per-launch HBM traffic of `kernel` from the committed rocprofv3 PMC summary of this config
-    (profiles/r<N>/pmc_<config>.json, made by tools/profile.sh + tools/pmc_summary.py: separate
-    FETCH_SIZE and WRITE_SIZE passes over the same bench command), scaled to this run's events per
-    launch. Returns (raw FETCH+WRITE bytes, bytes with FETCH doubled per the gfx950 streaming-read
-    correction, source) or None."""
-    for rnd in ("r4", "r3", "r2", "r1"):  # the latest round's summary of this config
+    """Per-launch HBM traffic of `kernel` from the committed rocprofv3 PMC summary of this exact line
+    (profiles/r<N>/pmc_<pmc_tag>.json, made by `tools/gpu.sh prof <pmc_tag> <bench args>`: separate
+    FETCH_SIZE and WRITE_SIZE passes over the same bench command, summarized by tools/pmc_summary.py),
+    scaled to this run's events per launch. None when this line has no summary of its own (a
+    variant's traffic is never borrowed from another line's). Returns (raw FETCH+WRITE bytes, bytes
+    with FETCH doubled per the gfx950 streaming-read correction, source) or None."""
+    for rnd in ("r5", "r4", "r3", "r2", "r1"):  # the latest round's summary of this config
         path = os.path.join(ROOT, "profiles", rnd, "pmc_%s.json" % config)
         if os.path.exists(path):
             break
     else:
         return None
     with open(path) as f:
-        k = json.load(f)["kernels"].get(kernel)
+        ks = json.load(f)["kernels"]
+    k = ks.get(kernel) or ks.get(kernel.split("<")[0])  # (earlier rounds' summaries: untemplated names)
     if not k:
         return None
     scale = events_per_launch / max(k["grid"], 1)
@@ -809,7 +824,7 @@ def main():
             if per_event:
                 bytes_launch = int(per_event * ev_per_launch)
                 achieved = bytes_launch / (us * 1e-6) / 1e9
-                tr = pmc_traffic(cfg, kname, ev_per_launch)
+                tr = pmc_traffic(pmc_tag(args), kname, ev_per_launch)
                 roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
                              "alg_bytes_per_launch": bytes_launch, "traffic": tr[0] if tr else None,
                              "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None})

@@ -492,10 +492,11 @@ def test_fused_overflow_bound_retightened_at_checkpoints():
 @pytest.mark.parametrize("order", ["random", "reversed"])
 def test_fused_claim_mode_ids_that_do_not_rise(order):
     """Ids that do not rise (the reference benchmark's random and reversed IdPermutation): the fused
-    pass runs in claim mode (one key-map claim per id that reaches the exists check, tagged apart from
-    the general path's epochs), records hashed. A window with an in-window duplicate id leaves the
-    class (the second claimant) and goes to the general path; retries of stored ids are exists codes;
-    a rising window after them commits with claims and switches back to the rising-id test."""
+    pass runs in claim mode (each id that reaches the exists check claims its entry in the transfer
+    table, pointing at its in-place record), records hashed. A window with an in-window duplicate id
+    leaves the class (the second claimant) and goes to the general path (every claim removed first);
+    retries of stored ids are exists codes; a rising window after them commits with claims and switches
+    back to the rising-id test."""
     n_acc = 2000
     gpu, ref = _engines(n_acc, 1 << 20)
     code = workload.ID_ORDERS[order]
@@ -531,6 +532,69 @@ def test_fused_claim_mode_ids_that_do_not_rise(order):
         _check(gpu, ref, _window(first + 2 * 10**7, n_acc, seed=34))
         st = gpu.stats()
         assert st["fused_windows"] >= 5
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_fused_claim_mode_moves_aborts_and_lookups():
+    """Claim mode with records that move (static failures early in each window: the claims of the
+    records after them are re-pointed to their ranks), an id whose first event fails before the exists
+    check and whose second commits (not a duplicate, as in the reference: the failed event stored
+    nothing), a window that leaves the class after its claims were made (every claim removed, the
+    general path commits it), retries of moved records (exists codes through the re-pointed claims) and
+    a lookup of every id: equal to the restatement throughout."""
+    n_acc = 2000
+    gpu, ref = _engines(n_acc, 1 << 20)
+    rng = np.random.default_rng(17)
+    code = workload.ID_ORDERS["random"]
+    try:
+        _accounts(gpu, ref, n_acc)
+        first = 0
+        committed = []
+
+        def win(seed=41):
+            nonlocal first
+            b = _window(first, n_acc, seed=seed)
+            first += WIN * BM
+            flat = np.concatenate(b)
+            ids = workload.permute_ids(flat.copy(), code, 7)
+            flat["id_lo"], flat["id_hi"] = ids["id_lo"], ids["id_hi"]
+            return [flat[k * BM:(k + 1) * BM].copy() for k in range(WIN)]
+
+        for w in range(4):
+            b = win()
+            _inject_static_failures(b, rng, n_acc)
+            if w == 2:
+                # event 5 of batch 3 fails (debit account not found); a later event reuses its id
+                b[3]["debit_account_id_lo"][5] = n_acc + 500
+                b[6]["id_lo"][9], b[6]["id_hi"][9] = b[3]["id_lo"][5], b[3]["id_hi"][5]
+            _check(gpu, ref, b)
+            committed.append(np.concatenate(b))
+        assert gpu.stats()["fused_windows"] == 4
+        # leaves the class in its last batch (a linked event): claims made, then removed
+        b = win()
+        b[7]["flags"][100] = 1  # linked (a chain of two)
+        _check(gpu, ref, b)
+        committed.append(np.concatenate(b))
+        assert gpu.stats()["fused_windows"] == 4
+        for w in range(3):  # back-off, then claim mode again with retries of moved records
+            b = win()
+            if w == 2:
+                old = committed[1][BM:BM + 300].copy()
+                old["amount_lo"][::5] += 1
+                b[2][:300] = old
+            _check(gpu, ref, b)
+            committed.append(np.concatenate(b))
+        assert gpu.stats()["fused_windows"] >= 5
+        allx = np.concatenate(committed)
+        for f in range(0, len(allx), BM):  # (a lookup batch holds batch_max ids)
+            q = np.zeros(min(BM, len(allx) - f), [("lo", "<u8"), ("hi", "<u8")])
+            q["lo"], q["hi"] = allx["id_lo"][f:f + len(q)], allx["id_hi"][f:f + len(q)]
+            assert gpu.commit(0, 99, 0, Operation.lookup_transfers, q.tobytes()) == \
+                ref.commit(0, 99, 0, Operation.lookup_transfers, q.tobytes()), f
         _compare_final(gpu, ref)
     finally:
         gpu.close()

@@ -38,6 +38,7 @@ static_assert(sizeof(AccEntry) == 32, "AccEntry");
 
 typedef unsigned long long XEntry;  // [63:32] high half of the id hash, [31:0] record slot
 #define X_EMPTY 0xFFFFFFFFFFFFFFFFull  // slot NONE32 never occurs in a live entry
+#define X_TOMB 0xFFFFFFFFFFFFFFFEull   // a removed entry (the fused pass's claims, fused.h): probed past, never matched
 
 // Window-local key map. Entries are epoch-tagged (the window number), so a stale entry from an
 // earlier window reads as empty and nothing is ever reset. Keys are never stored: `key` names the
@@ -112,8 +113,9 @@ struct __attribute__((aligned(64))) Globals {
   uint64_t cpw_events_total;  // cumulative W events decided by component walkers
   uint32_t small_win;   // this window: ovf_bound + window amounts < 2^64 (set by k_walk; k_final reads it)
   uint32_t cold_count;  // hot ranks found non-binding this window (k_bind_decide; k_bind_finish resets)
-  // Sorted transfer prefix: records [0, x_sorted) have ids < 2^64, strictly increasing with the
-  // slot, and are not in the hash table (found by binary search, x_prefix_find). A window whose
+  // Sorted transfer prefix: records [0, x_sorted) have ids strictly increasing (u128 order) with the
+  // slot, and are found by binary search (x_prefix_find; the hash table holds some of them too when a
+  // claim-mode fused window extended the prefix: the same slots either way). A window whose
   // ids are strictly increasing and above every stored id extends it instead of hashing its inserts
   // (monotonic ids, the form TigerBeetle recommends); the first other window freezes it.
   uint64_t x_sorted;
@@ -154,7 +156,9 @@ struct __attribute__((aligned(64))) Globals {
   // (reserved per block in FuScratch::slots, written by k_fu_final)
   uint64_t fu_exp_base;
   uint32_t sh_cap_bad;  // sharded order-free window: some shard's store lacks room for its inserts (k_sh_decide)
-  uint32_t pad8;
+  uint32_t fu_done;     // blocks of k_fu_final<true> finished (the last copies the reply out, fused.h)
+  uint32_t fu_claim;    // the fused window ran in claim mode (its events claimed their ids in the table)
+  uint32_t pad9;
 };
 
 // The fused pass (fused.h) committed this window: the general path's kernels return at once.
@@ -268,13 +272,16 @@ __device__ inline uint32_t acc_find(const AccEntry* __restrict__ tab, uint64_t m
 }
 
 // Continues a transfer-id probe whose first entry `e` (at h & mask) is already loaded.
+// slot_lim: entries at or past it are passed over (the fused pass's undo: the claims of the window
+// being undone, fused.h).
 __device__ inline uint32_t x_probe_from(const XEntry* __restrict__ tab, const tb_transfer_t* __restrict__ xr,
-                                        uint64_t mask, uint64_t h, XEntry e, tb_uint128_t id) {
+                                        uint64_t mask, uint64_t h, XEntry e, tb_uint128_t id,
+                                        uint64_t slot_lim = ~0ull) {
   const uint32_t fp = (uint32_t)(h >> 32);
   uint64_t pos = h & mask;
   for (;;) {
     if (e == X_EMPTY) return NONE32;
-    if ((uint32_t)(e >> 32) == fp) {
+    if ((uint32_t)(e >> 32) == fp && e != X_TOMB && (uint32_t)e < slot_lim) {
       const tb_uint128_t k = xr[(uint32_t)e].id;
       if (k.lo == id.lo && k.hi == id.hi) return (uint32_t)e;
     }
@@ -334,13 +341,6 @@ __device__ inline uint32_t x_prefix_find(const tb_transfer_t* __restrict__ xr, u
 // Whether `id` can be in the transfer table (x_id_max bounds every stored id).
 __device__ inline bool x_may_exist(const tb_uint128_t& id, u128 x_id_max) { return U(id) <= x_id_max; }
 __device__ inline u128 umax128(u128 a, u128 b) { return a > b ? a : b; }
-// Raises a u128 upper bound with two 64-bit atomics: the word-wise maximum is >= every value offered
-// (for rare paths: open, sharded apply); the hot paths fold exact per-block maxima instead.
-__device__ inline void atomic_bound_u128(u128* p, u128 v) {
-  unsigned long long* w = reinterpret_cast<unsigned long long*>(p);
-  atomicMax(w, (unsigned long long)v);
-  atomicMax(w + 1, (unsigned long long)(v >> 64));
-}
 // Wave-wide max of a u128 (every lane gets it).
 __device__ inline u128 wave_max_u128(u128 v) {
 #pragma unroll
@@ -371,6 +371,50 @@ __device__ inline void acc_insert(AccEntry* tab, uint64_t mask, tb_uint128_t id,
 
 // Inserts a distinct, absent id whose record is already stored at xr[slot] (readers run in later
 // kernels): one 64-bit CAS.
+// The fused pass's claim of a transfer id (fused.h, claim mode): walks the id's probe sequence from
+// entry e at h. A stored transfer with the id (slot below `base`) is returned; an entry of this
+// window's own events (slot base + j, compared against the request's event j) marks an in-window
+// duplicate (*dup); at the sequence's first empty entry the event claims it for its own record
+// (fp | base + i) when `insert`, and NONE32 is returned.
+// *cpos: the position of the event's claim (NONE32: none), where k_fu_final finds it again.
+__device__ inline uint32_t x_probe_claim(XEntry* tab, const tb_transfer_t* __restrict__ xr,
+                                         const tb_transfer_t* __restrict__ ev, uint64_t mask, uint64_t h, XEntry e,
+                                         tb_uint128_t id, uint64_t base, uint32_t i, uint32_t E, bool insert,
+                                         bool* dup, uint32_t* cpos) {
+  const uint32_t fp = (uint32_t)(h >> 32);
+  uint64_t pos = h & mask;
+  *dup = false;
+  *cpos = NONE32;
+  for (;;) {
+    if (e == X_EMPTY) {
+      if (!insert) return NONE32;
+      const XEntry mine = ((unsigned long long)fp << 32) | (uint32_t)(base + i);
+      const XEntry seen = atomicCAS(&tab[pos], X_EMPTY, mine);
+      if (seen == X_EMPTY) {
+        *cpos = (uint32_t)pos;
+        return NONE32;
+      }
+      e = seen;  // another claim took it first: examine that one
+      continue;
+    }
+    if (e != X_TOMB && (uint32_t)(e >> 32) == fp) {
+      const uint32_t slot = (uint32_t)e;
+      if (slot < base) {
+        const tb_uint128_t k = xr[slot].id;
+        if (k.lo == id.lo && k.hi == id.hi) return slot;
+      } else if (slot - base < E) {
+        const tb_uint128_t k = ev[slot - base].id;
+        if (k.lo == id.lo && k.hi == id.hi) {
+          *dup = true;
+          return NONE32;
+        }
+      }
+    }
+    pos = (pos + 1) & mask;
+    e = tab[pos];
+  }
+}
+
 __device__ inline void x_insert(XEntry* tab, uint64_t mask, tb_uint128_t id, uint32_t slot) {
   const uint64_t h = hash_id(id.lo, id.hi);
   const XEntry v = ((unsigned long long)(uint32_t)(h >> 32) << 32) | slot;

@@ -1663,15 +1663,23 @@ __global__ void __launch_bounds__(256) k_copy_in(uint4* __restrict__ dst, const 
   for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n16; k += gridDim.x * 256) dst[k] = src[k];
 }
 // The Globals ([0, g16) words) and, with the reply, the reply block at H_REPLY_OFF (its count and the
-// first min(count, n_max) results): the same layout on both sides.
+// first min(count, n_max) results): the same layout on both sides. flag (one block only): written
+// with `seq` after every word, for the host to poll (reply_flag_out).
+__device__ inline void reply_flag_out(unsigned long long* flag, unsigned long long seq) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __global__ void __launch_bounds__(256) k_reply_out(const uint4* __restrict__ dev, uint4* __restrict__ host, uint32_t g16,
-                                                   uint32_t reply16, uint32_t n_max, uint32_t with_reply) {
+                                                   uint32_t reply16, uint32_t n_max, uint32_t with_reply,
+                                                   unsigned long long* flag, unsigned long long seq) {
   const uint32_t c = with_reply ? min(*reinterpret_cast<const uint32_t*>(dev + reply16), n_max) : 0u;
   const uint32_t r16 = with_reply ? 1u + (c * 8u + 15u) / 16u : 0u;
   for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < g16 + r16; k += gridDim.x * 256) {
     const uint32_t j = k < g16 ? k : reply16 + (k - g16);
     host[j] = dev[j];
   }
+  if (flag) reply_flag_out(flag, seq);
 }
 
 // Harness `setup` (state_machine.zig:2545-2561).

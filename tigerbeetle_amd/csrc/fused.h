@@ -62,46 +62,31 @@ struct FuEv {
   unsigned long long amount;  // C_REACH events: the amount (every one counts toward the overflow bound)
   u128 id_key;                // C_REACH events: the id (x_id_max bound)
   uint64_t expires_at;        // a pending create with a timeout: its expiry (0 = none)
+  uint32_t cpos;              // claim mode: the table position of the event's claim (NONE32: none)
   bool simple, reach, pending;
 };
 
-// Claim mode (windows whose ids are not known to rise: Globals::mono_prev = 0): the ids that reach
-// the exists check claim a key-map entry tagged FU_CLAIM | epoch (never a general-path epoch, so a
-// window that leaves the class and goes to the general path finds them stale); a second claimant of
-// the same id is an in-window duplicate (outside the class). Returns whether `id` was already claimed
-// by another event.
-#define FU_CLAIM 0x80000000u
-__device__ __forceinline__ bool fu_claim(BEntry* bm, uint32_t mask, const uint8_t* ev, tb_uint128_t id, uint32_t i,
-                                         uint32_t tag) {
-  uint32_t h = (uint32_t)hash_id(id.lo, id.hi) & mask;
-  for (;;) {
-    unsigned long long old = __hip_atomic_load(&bm[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-      if (bk_epoch(old) != tag) {
-        const unsigned long long prev = atomicCAS(&bm[h].key, old, ((unsigned long long)tag << 32) | i);
-        if (prev == old) return false;
-        old = prev;
-        continue;
-      }
-      const tb_uint128_t k = bkey(ev, bk_owner(old), 0);
-      if (k.lo != id.lo || k.hi != id.hi) break;  // another id: probe on
-      return bk_owner(old) != i;
-    }
-    h = (h + 1) & mask;
-  }
-}
+// Claim mode (windows whose ids are not known to rise: Globals::mono_prev = 0): an event that reaches
+// the exists check claims its id in the transfer table itself (x_probe_claim: its entry points at its
+// in-place record, slot base + i), so one probe sequence finds a stored transfer, finds an in-window
+// duplicate (another event's claim: outside the class) and indexes the new record. k_fu_final re-points
+// the claims of records that move down to their ranks (by the claim's position, fs.cpos: never by a
+// search, which could meet another record's re-pointed entry), and removes every claim of a window
+// that leaves the class. (Round 4 claimed in the window key map and inserted into the table after the
+// window: two random probe sequences per event.)
 
-// prev_id: the id of event i - 1 (i > 0). ts: the event's timestamp (the record as inserted). claim:
-// claim mode (bm, bmask, tag), else the ids must rise.
+// prev_id: the id of event i - 1 (i > 0). ts: the event's timestamp (the record as inserted). base:
+// the window's first record slot. claim: claim mode (ev: the window's events, E of them), else the
+// ids must rise. undo (k_fu_final): the same decision again, the window's own claims passed over.
 __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id, const tb_transfer_t& t, uint64_t ts,
-                                          u128 x_id_max, uint64_t P, FuEv* o, bool claim = false,
-                                          BEntry* bm = nullptr, uint32_t bmask = 0, const uint8_t* evb = nullptr,
-                                          uint32_t tag = 0) {
+                                          u128 x_id_max, uint64_t P, uint64_t base, FuEv* o, bool claim = false,
+                                          const tb_transfer_t* ev = nullptr, uint32_t E = 0, bool undo = false) {
   const uint16_t f = t.flags;
   o->dr = o->cr = NONE32;
   o->amount = 0;
   o->id_key = 0;
   o->expires_at = 0;
+  o->cpos = NONE32;
   o->reach = false;
   o->pending = (f & TB_TRANSFER_PENDING) != 0;
   // no chain, no post/void; claim-free (ids strictly increasing over the window, k_ct_prep's test)
@@ -126,12 +111,8 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
           const bool mx = x_may_exist(t.id, x_id_max);
           const uint64_t hx = hash_id(t.id.lo, t.id.hi);
           const AccEntry ed = d.acc_tab[hd], ec = d.acc_tab[hc];
-          const XEntry ex = mx ? d.x_tab[hx & d.x_mask] : X_EMPTY;
-          // claim mode: the claim goes out behind the probes' first loads (one counter orders a
-          // wave's loads and atomics: issued earlier, the returning atomic would hold up their use).
-          // An event that then fails the account checks has claimed its id too: a later duplicate of
-          // it sends the window to the general path, which decides it exactly.
-          const bool dup = claim && fu_claim(bm, bmask, evb, t.id, i, tag);
+          // (claim mode probes whether or not the id may exist: its claim indexes the new record)
+          const XEntry ex = (mx || claim) ? d.x_tab[hx & d.x_mask] : X_EMPTY;
           AccEntry de, ce;
           o->dr = acc_probe_from(d.acc_tab, d.acc_mask, hd, ed, t.debit_account_id, &de);
           o->cr = acc_probe_from(d.acc_tab, d.acc_mask, hc, ec, t.credit_account_id, &ce);
@@ -149,19 +130,26 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
             if (((de.flags | ce.flags) & TB_ACCOUNT_HISTORY) || (de.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) ||
                 (ce.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) || t.amount.hi != 0 || t.amount.lo >= FU_AMOUNT_MAX)
               simple = false;
-            if (dup) simple = false;  // in-window duplicate
-            uint32_t xs = mx ? x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id) : NONE32;
-            if (xs == NONE32 && mx) xs = x_prefix_find(d.xr, P, t.id);
-            // :1506-1507; then the balance tail (:1509-1547): its overflow checks cannot fail here (the
-            // amounts and the bound, above), the timeout's can (a single-phase create has timeout 0)
-            code = xs != NONE32 ? ct_exists(t, d.xr[xs]) : (uint32_t)TB_CT_OK;
-            if (code == TB_CT_OK && t.timeout != 0) {
-              const uint64_t tns = (uint64_t)t.timeout * TB_NS_PER_S;
-              if (ovf64(ts, tns))
-                code = TB_CT_OVERFLOWS_TIMEOUT;
-              else
-                o->expires_at = ts + tns;
+            // the balance tail (:1509-1547) after exists: its overflow checks cannot fail here (the
+            // amounts and the bound, above), the timeout's can (a single-phase create has timeout 0);
+            // computed first, so that an event failing it claims nothing
+            const uint64_t tns = (uint64_t)t.timeout * TB_NS_PER_S;
+            const bool tovf = t.timeout != 0 && ovf64(ts, tns);
+            uint32_t xs = NONE32;
+            if (claim) {
+              // the sorted prefix first (a transfer found there is not in the table), then the claim
+              if (mx) xs = x_prefix_find(d.xr, P, t.id);
+              bool dup = false;
+              if (xs == NONE32)
+                xs = x_probe_claim(d.x_tab, d.xr, ev, d.x_mask, hx, ex, t.id, base, i, E, !tovf, &dup, &o->cpos);
+              if (dup) simple = false;  // in-window duplicate
+            } else {
+              xs = mx ? x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id, undo ? base : ~0ull) : NONE32;
+              if (xs == NONE32 && mx) xs = x_prefix_find(d.xr, P, t.id);
             }
+            // :1506-1507
+            code = xs != NONE32 ? ct_exists(t, d.xr[xs]) : (tovf ? (uint32_t)TB_CT_OVERFLOWS_TIMEOUT : (uint32_t)TB_CT_OK);
+            if (code == TB_CT_OK && t.timeout != 0) o->expires_at = ts + tns;
           }
         }
       }
@@ -191,6 +179,7 @@ struct FuScratch {
   unsigned long long* pto;  // per wave: ok pending creates with a timeout the expiry scan can see
   unsigned long long* pnmin;  // per block: smallest expiry of its ok creates with a timeout (~0: none)
   uint32_t* pbase;          // per block: its first live expiry entry within its slot (fu_slot_base)
+  uint32_t* cpos;           // per event, claim mode: its claim's table position (NONE32: none)
   unsigned long long* slots;  // FU_SLOTS failure counts, then FU_SLOTS expiry-entry counts (epoch_count_add)
 };
 
@@ -239,6 +228,10 @@ __device__ __forceinline__ void fu_store_records(Dev d, const uint4* src, bool o
 
 // Decide, apply, store in place. Writes nothing but scratch, the in-place records and statuses (slots
 // at or beyond the store's end) and, when its events are simple, the balance adds.
+// HOST (the synchronous path): `ev` is the request in pinned host memory, copied through to ev_copy
+// (below). (Issuing all eight of a lane's 16 B loads before the first use measured slower: 43 against
+// 38 us per 8190-event batch.)
+template <bool HOST>
 __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
                                                    WinDesc w, uint32_t epoch, uint32_t fo_only, uint32_t* fmark,
                                                    uint32_t pn_skip, uint4* __restrict__ ev_copy) {
@@ -265,7 +258,7 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   // by this pass, which stores it to ev_copy in HBM as it goes (every later kernel and a replay read
   // that), whatever the window's fate, instead of a separate copy launch ahead of it. A wave that does
   // not decide copies its 64 records here.
-  if (ev_copy && aborted) {
+  if (HOST && aborted) {
     const uint32_t i0 = k * FU_T + wave * 64;
     const uint32_t n16 = i0 < w.E ? min(64u, w.E - i0) * 8u : 0u;
     const uint4* src = reinterpret_cast<const uint4*>(ev + i0);
@@ -303,6 +296,7 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
     g->fu_epoch = epoch;
     g->fu_base = base;
     g->fu_exp_base = g->exp_count;  // (unchanged until k_fu_final's last block)
+    g->fu_claim = claim ? 1u : 0u;  // (k_fu_final re-points or removes this window's claims)
     // the window may extend the sorted prefix (first id above every stored id; its ids must rise
     // too: Globals::fu_nonmono, k_fu_final)
     g->fu_prefix = (P == base && U(ev[0].id) > x_id_max) ? 1u : 0u;
@@ -334,7 +328,7 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
         if (r < nrec) {
           const uint4 v = ld_stream(src + r * 8 + half * 4 + q);
           ws[r * 4 + (q ^ ((r >> 2) & 3))] = v;
-          if (ev_copy) ev_copy[(size_t)(i0 + r) * 8 + half * 4 + q] = v;
+          if (HOST) ev_copy[(size_t)(i0 + r) * 8 + half * 4 + q] = v;
         }
       }
       wave_sync();
@@ -351,11 +345,13 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
   fe.expires_at = 0;
   if (i < E && !aborted) {
     const uint64_t ts = win_ts(w, win_batch(w, i), i);  // :1253 (the record as inserted)
-    fu_decide(d, i, prev, t, ts, x_id_max, P, &fe, claim, s.bmap, s.bmask, reinterpret_cast<const uint8_t*>(ev),
-              FU_CLAIM | epoch);
+    fu_decide(d, i, prev, t, ts, x_id_max, P, base, &fe, claim, ev, E);
     nonmono = i > 0 && !(U(t.id) > prev);
     t.timestamp = ts;
   }
+  // claim mode: every event's claim position (NONE32 where it made none: a wave that skipped its
+  // decisions too), for k_fu_final
+  if (claim && i < E) fs.cpos[i] = aborted ? NONE32 : fe.cpos;
   const bool blk_simple = __syncthreads_and(fe.simple && !aborted) && glob_ok;
   if (threadIdx.x == 0) {
     fs.applied[k] = blk_simple ? 1 : 0;
@@ -448,8 +444,9 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
 // totals into Globals.
 // fo_only: the general path was not launched for this window (host.inc launch_window); a window
 // outside the class then stops every later window (window_error bit 3) until the host replays them.
-__global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
-                                                   WinDesc w, uint32_t epoch, FinalOut o, uint32_t fo_only) {
+__device__ __forceinline__ void fu_final_body(const Dev& d, const Scratch& s, const FuScratch& fs,
+                                              const tb_transfer_t* __restrict__ ev, const WinDesc& w, uint32_t epoch,
+                                              const FinalOut& o, uint32_t fo_only) {
   __shared__ uint4 stage[FU_T * 4];
   __shared__ uint32_t lds[FU_T / 64];
   __shared__ unsigned long long red[FU_T / 64];
@@ -473,11 +470,19 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
         atomicOr(&g->window_error, 8u);
       }
     }
-    if (!fs.applied[k] || i >= E) return;
+    if (i >= E) return;
+    // claim mode: every claim of the window removed (blocks that applied or not), before the general
+    // path sees the table
+    if (g->fu_claim) {
+      const uint32_t p = fs.cpos[i];
+      if (p != NONE32) d.x_tab[p] = X_TOMB;
+    }
+    if (!fs.applied[k]) return;
     FuEv fe;
-    // (no claims: the undo needs the codes, amounts, fields and accounts only)
+    // (no claims: the undo needs the codes, amounts, fields and accounts only; the window's own claims
+    // are passed over, so each event finds what it found before)
     fu_decide(d, i, i > 0 ? U(ev[i - 1].id) : (u128)0, ev[i], win_ts(w, win_batch(w, i), i), g->x_id_max,
-              g->x_sorted, &fe);
+              g->x_sorted, g->fu_base, &fe, false, nullptr, 0, true);
     if (fe.code == TB_CT_OK) {
       (void)atomicAdd(fu_dr_field(d, fe), 0ull - fe.amount);
       (void)atomicAdd(fu_cr_field(d, fe), 0ull - fe.amount);
@@ -543,7 +548,17 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
     const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, (int)__builtin_ctzll(okm));
     fu_store_records(d, rec, ok, okm, base + r0, stage + wave * 256);
   }
-  if (ok && !prefix_win) x_insert(d.x_tab, d.x_mask, ev[i].id, (uint32_t)(base + rins));
+  if (g->fu_claim) {
+    // claim mode: the ok events' claims index their records already (in a window that extends the
+    // sorted prefix too: a record found by both finds the same slot); a record that moved down to its
+    // rank is re-pointed
+    if (ok && rins != i) {
+      const uint32_t p = fs.cpos[i];  // (an ok event of a committed claim window made its claim)
+      d.x_tab[p] = (d.x_tab[p] & 0xFFFFFFFF00000000ull) | (uint32_t)(base + rins);
+    }
+  } else if (ok && !prefix_win) {
+    x_insert(d.x_tab, d.x_mask, ev[i].id, (uint32_t)(base + rins));
+  }
   if (__syncthreads_or(pto)) {
     // live expires_at entries of the window's pending creates with a timeout, in event order, at this
     // block's reservation (k_ct_fused): after the entries of the slots before its own
@@ -619,6 +634,38 @@ __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch f
       g->sp_done = 1;
       g->sp_fails = 0;
       g->fu_windows++;
+    }
+  }
+}
+
+// The synchronous path's reply (HOST, a fused-only batch): the block that finishes last copies the
+// Globals and the reply block (count and results) to pinned host memory through its device mapping,
+// as k_reply_out does in its own launch on the other paths (host.inc reply_out).
+struct ReplyOut {
+  uint4* host;       // h_pinned's device mapping
+  uint32_t g16;      // Globals words
+  uint32_t reply16;  // the reply block's first word (H_REPLY_OFF / 16), the same on both sides
+  uint32_t n_max;
+  unsigned long long* flag;  // written with seq after every word (the host polls it)
+  unsigned long long seq;
+};
+template <bool HOST>
+__global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
+                                                   WinDesc w, uint32_t epoch, FinalOut o, uint32_t fo_only, ReplyOut ro) {
+  fu_final_body(d, s, fs, ev, w, epoch, o, fo_only);
+  if (HOST) {
+    __shared__ uint32_t last;
+    if (last_block_done(&d.g->fu_done, &last)) {
+      const uint4* dev = reinterpret_cast<const uint4*>(d.g);
+      const uint32_t c = min(*reinterpret_cast<const volatile uint32_t*>(dev + ro.reply16), ro.n_max);
+      const uint32_t words = ro.g16 + 1u + (c * 8u + 15u) / 16u;
+      for (uint32_t k = threadIdx.x; k < words; k += FU_T) {
+        const uint32_t j = k < ro.g16 ? k : ro.reply16 + (k - ro.g16);
+        ro.host[j] = dev[j];
+      }
+      __threadfence_system();
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(ro.flag, ro.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }

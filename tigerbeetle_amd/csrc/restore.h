@@ -36,12 +36,36 @@ __global__ void __launch_bounds__(256) k_load_accounts(Dev d, uint64_t first, ui
   }
 }
 
-__global__ void __launch_bounds__(256) k_load_transfers(Dev d, uint64_t first, uint64_t n) {
+// Exact bounds on the stored ids (Globals::x_id_max) from the rare bulk paths (open, the sharded
+// general path's applies): each block of a grid of at most IDMAX_BLOCKS 256-thread blocks stores its
+// maximum, and the one-block finishing kernel folds them (a word-wise pair of 64-bit atomics would
+// give (max hi, max lo): far above the true maximum with time-based ids, whose low words are random).
+#define IDMAX_BLOCKS 4096u
+__device__ inline void block_idmax_out(u128 v, u128* out) {
+  __shared__ u128 l[4];
+  v = wave_max_u128(v);
+  if ((threadIdx.x & 63) == 0) l[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = umax128(umax128(l[0], l[1]), umax128(l[2], l[3]));
+}
+// The maximum of nblk block maxima, in thread 0 of a 256-thread block (every thread calls it).
+__device__ inline u128 fold_idmax(const u128* in, uint32_t nblk) {
+  __shared__ u128 l[4];
+  u128 m = 0;
+  for (uint32_t j = threadIdx.x; j < nblk; j += 256) m = umax128(m, in[j]);
+  m = wave_max_u128(m);
+  if ((threadIdx.x & 63) == 0) l[threadIdx.x >> 6] = m;
+  __syncthreads();
+  return umax128(umax128(l[0], l[1]), umax128(l[2], l[3]));
+}
+
+__global__ void __launch_bounds__(256) k_load_transfers(Dev d, uint64_t first, uint64_t n, u128* idmax) {
+  u128 m = 0;
   for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t slot = first + k;
     const tb_transfer_t t = d.xr[slot];
     x_insert(d.x_tab, d.x_mask, t.id, (uint32_t)slot);
-    atomic_bound_u128(&d.g->x_id_max, U(t.id));
+    m = umax128(m, U(t.id));
     if (!(t.flags & TB_TRANSFER_PENDING) || t.timeout == 0 || d.xstatus[slot] != TB_PENDING_PENDING) continue;
     const uint64_t expires_at = expires_at_of(t);
     if ((t.timestamp >> 63) || expires_at > TB_TIMESTAMP_MAX) continue;  // never visible to the scan
@@ -52,6 +76,7 @@ __global__ void __launch_bounds__(256) k_load_transfers(Dev d, uint64_t first, u
     const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), 1ull);
     d.exp[*d.exp_cur][q] = e;
   }
+  block_idmax_out(m, idmax);
 }
 
 // The account_balances groove's rows (sorted by timestamp): each lands on the slot of the transfer
@@ -76,8 +101,12 @@ __global__ void __launch_bounds__(256) k_load_history(Dev d, const tb_account_ba
   }
 }
 
-__global__ void k_load_finish(Dev d, const LoadBound* lb, uint64_t n_acc, uint64_t n_x) {
+__global__ void __launch_bounds__(256) k_load_finish(Dev d, const LoadBound* lb, uint64_t n_acc, uint64_t n_x,
+                                                     const u128* idmax, uint32_t nblk) {
+  const u128 m = fold_idmax(idmax, nblk);
+  if (threadIdx.x != 0) return;
   Globals* g = d.g;
+  if (m > g->x_id_max) g->x_id_max = m;
   g->acc_count = n_acc;
   g->x_count = n_x;
   g->x_sorted = 0;  // every loaded transfer is hashed

@@ -239,6 +239,14 @@ enum : uint32_t { ZW_CODE = 0x3F, ZW_STATIC = 0x40, ZW_LINKED = 0x80, ACC_DR_LIM
 static_assert(TB_CT_EXCEEDS_DEBITS + 1 <= (int)ZW_CODE && TB_CA_EXISTS + 1 <= (int)ZW_CODE, "codes fit 6 bits");
 enum : uint32_t { SHX_UNSUP = 16 };
 #define SH_SCAN_T 256  // k_sh_scan's block: small blocks keep more of its latency-bound waves resident
+// Resident waves per SIMD requested for k_sh_scan / the unstaged k_sh_apply (0: the compiler's choice);
+// A/B builds override them (tools/variants.sh -D...).
+#ifndef SH_SCAN_WPE
+#define SH_SCAN_WPE 0
+#endif
+#ifndef SH_APPLY_WPE
+#define SH_APPLY_WPE 8
+#endif
 
 __device__ inline bool sh_verdict(const XchView& x) { return x.trailer[x.par] != 0; }
 
@@ -257,9 +265,10 @@ __device__ inline bool sh_verdict(const XchView& x) { return x.trailer[x.par] !=
 // ~8 us + a launch gap per window; per-block returning atomics on Globals words ~50 us per 1M events.)
 // ------------------------------------------------------------------------------------------------
 template <bool XFER>
-__global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes,
+__global__ void __launch_bounds__(SH_SCAN_T) __attribute__((amdgpu_waves_per_eu(SH_SCAN_WPE))) k_sh_scan(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes,
                                                        WinDesc w, uint32_t epoch, XchView xch, uint32_t G, uint32_t me) {
   __shared__ u128 red[SH_SCAN_T / 64];
+  __shared__ u128 redm[SH_SCAN_T / 64];
   __shared__ uint32_t aux;
   const uint32_t i = blockIdx.x * SH_SCAN_T + threadIdx.x;
   const uint32_t E = w.E;
@@ -285,16 +294,23 @@ __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const u
   // the previous fast-path window's ids did not all rise: claims find in-window duplicates
   const bool claim = !XFER || g->mono_prev == 0;
   uint32_t roles = 0, zw = 0, accb = 0;
-  u128 amount = 0;
+  uint32_t dslot = NONE32, cslot = NONE32;  // this shard's account slots (NONE32: not owned or missing)
+  u128 amount = 0, idm = 0;
   bool owned_id = false;
+  uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
   if (i < E) {
+    // per-lane 16 B loads of the record head (staging the wave's heads through LDS, four lanes per
+    // record, measured slower: 51 against 40 us per 1M-event window at G = 8)
     const uint4* q = reinterpret_cast<const uint4*>(ev_bytes + (size_t)i * 128);
-    const tb_uint128_t id = rw_u128(q[0]);
-    if (shard_of(id.lo, id.hi, G) == me) roles |= ROLE_ID;
-    uint4 q1 = make_uint4(0, 0, 0, 0), q2 = q1;
+    q0 = q[0];
     if (XFER) {
       q1 = q[1];
       q2 = q[2];
+      q3 = q[3];
+    }
+    const tb_uint128_t id = rw_u128(q0);
+    if (shard_of(id.lo, id.hi, G) == me) roles |= ROLE_ID;
+    if (XFER) {
       const tb_uint128_t dra = rw_u128(q1), cra = rw_u128(q2);
       if (shard_of(dra.lo, dra.hi, G) == me) roles |= ROLE_DR;
       if (shard_of(cra.lo, cra.hi, G) == me) roles |= ROLE_CR;
@@ -319,6 +335,7 @@ __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const u
             if (xs == NONE32) xs = x_prefix_find(d.xr, g->x_sorted, t.id);
           }
           code = xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]);
+          idm = U(t.id);  // (an owned id that may be inserted: k_sh_decide folds the bound on x_id_max)
         }
       } else {
         const tb_account_t a = reinterpret_cast<const tb_account_t*>(ev_bytes)[i];
@@ -337,14 +354,14 @@ __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const u
     }
     if (XFER && (roles & (ROLE_DR | ROLE_CR))) {
       // every amount an account owner sees counts toward the overflow bound, valid event or not
-      amount = U(rw_u128(q[3]));
+      amount = U(rw_u128(q3));
       const uint32_t ledger = q[7].x;  // each side's state is against the event's ledger
 #pragma unroll
       for (uint32_t side = 0; side < 2; side++) {
         if (!(roles & (side ? ROLE_CR : ROLE_DR))) continue;
         AccEntry e;
         const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, rw_u128(side ? q2 : q1), &e);
-        (side ? s.cr_slot : s.dr_slot)[i] = slot;
+        (side ? cslot : dslot) = slot;
         uint32_t st = SH_ACC_MISSING;
         if (slot != NONE32) {
           st = e.ledger == ledger ? SH_ACC_OK : SH_ACC_MISMATCH;
@@ -366,7 +383,12 @@ __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const u
     }
     // every byte of this shard's copy: its owned facts, zero elsewhere (the sum is the union)
     xch.zw[i] = (uint8_t)zw;
-    if (XFER) xch.acc[i] = (uint8_t)accb;
+    if (XFER) {
+      xch.acc[i] = (uint8_t)accb;
+      // the owned sides' slots only (written and read densely for every event measured slower)
+      if (roles & ROLE_DR) s.dr_slot[i] = dslot;
+      if (roles & ROLE_CR) s.cr_slot[i] = cslot;
+    }
     s.bstatus[i] = (uint8_t)roles;
   }
   if ((uint64_t)(amount >> 64) != 0) atomicOr(&aux, (uint32_t)SHX_HUGE);
@@ -380,8 +402,10 @@ __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const u
     const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(v >> 64), o, 64);
     v += ((u128)hi << 64) | lo;
   }
+  if (XFER) idm = wave_max_u128(idm);
   if ((threadIdx.x & 63) == 0) {
     red[threadIdx.x >> 6] = v;
+    if (XFER) redm[threadIdx.x >> 6] = idm;
     if (c) atomicAdd(&aux, c << SHX_OWN_SHIFT);
   }
   __syncthreads();
@@ -392,6 +416,11 @@ __global__ void __launch_bounds__(SH_SCAN_T) k_sh_scan(Dev d, Scratch s, const u
     const uint32_t bits = aux & 31u, own = aux >> SHX_OWN_SHIFT;
     s.blk_amt[blockIdx.x] = tot;
     s.blk_aux[blockIdx.x] = bits;
+    if (XFER) {
+      u128 bm = redm[0];
+      for (int w2 = 1; w2 < SH_SCAN_T / 64; w2++) bm = umax128(bm, redm[w2]);
+      s.blk_idmax[blockIdx.x] = bm;
+    }
     // this block's verdicts (bytes of this shard's trailer word: [0] duplicate / unchecked
     // non-rising ids / mismatch slots full, [2] overflow bound, [3] outside the class; [1] capacity
     // is decided from the owned-id slots after the exchange)
@@ -433,28 +462,30 @@ template <bool XFER>
 __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes, WinDesc w,
                                                    XchView xch, uint32_t e0, uint32_t e1) {
   __shared__ uint32_t nbad, nins;
-  __shared__ u128 ldsm[SEG / 64];
   Globals* g = d.g;
   if (blockIdx.x == 0) {
     // k_sh_scan's partials folded (read by k_sh_apply and the next window; nothing else here reads
     // them), whatever the verdict: its blocks' flags and amounts, and every shard's owned inserts
     // against its room (the same capacity verdict on every shard)
     __shared__ uint32_t f_bits, f_cap;
-    __shared__ u128 f_red[SEG / 64];
+    __shared__ u128 f_red[SEG / 64], f_mx[SEG / 64];
     if (threadIdx.x == 0) f_bits = f_cap = 0;
     __syncthreads();
     const uint32_t nblk = (w.E + SH_SCAN_T - 1) / SH_SCAN_T;
     uint32_t fb = 0;
-    u128 fa = 0;
+    u128 fa = 0, fm = 0;
     for (uint32_t j = threadIdx.x; j < nblk; j += SEG) {
       fb |= s.blk_aux[j];
-      if (XFER) fa += s.blk_amt[j];
+      if (XFER) {
+        fa += s.blk_amt[j];
+        fm = umax128(fm, s.blk_idmax[j]);
+      }
     }
     if (fb) atomicOr(&f_bits, fb);
-    if (threadIdx.x < xch.G) {
-      uint64_t tot = 0;
-      for (uint32_t q = 0; q < SH_OWN_SLOTS; q++) tot += xch.own[threadIdx.x * SH_OWN_SLOTS + q];
-      if (tot > xch.room[threadIdx.x]) atomicOr(&f_cap, 1u);
+    // shard g's owned-id slots: wave g, one slot per lane
+    for (uint32_t sg = threadIdx.x >> 6; sg < xch.G; sg += SEG / 64) {
+      const uint32_t tot = wave_sum(xch.own[sg * SH_OWN_SLOTS + (threadIdx.x & 63)]);
+      if ((threadIdx.x & 63) == 0 && tot > xch.room[sg]) atomicOr(&f_cap, 1u);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -462,14 +493,24 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
       const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(fa >> 64), o, 64);
       fa += ((u128)hi << 64) | lo;
     }
-    if ((threadIdx.x & 63) == 0) f_red[threadIdx.x >> 6] = fa;
+    if (XFER) fm = wave_max_u128(fm);
+    if ((threadIdx.x & 63) == 0) {
+      f_red[threadIdx.x >> 6] = fa;
+      f_mx[threadIdx.x >> 6] = fm;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       const uint32_t bits = f_bits;
       g->sh_cap_bad = f_cap;
       if (XFER) {
-        u128 amt = 0;
-        for (int q = 0; q < SEG / 64; q++) amt += f_red[q];
+        u128 amt = 0, mx = 0;
+        for (int q = 0; q < SEG / 64; q++) {
+          amt += f_red[q];
+          mx = umax128(mx, f_mx[q]);
+        }
+        // a bound on the stored ids (the owned ids that reached the exists check, inserted or not:
+        // an id above it cannot exist; the window's first id above it extends the sorted prefix)
+        if (mx > g->x_id_max) g->x_id_max = mx;
         g->batch_amount_sum += amt;
         if (bits & SHX_HUGE) g->batch_huge = 1;
         // every owned balance field stays below 2^64 this window: k_sh_apply's adds need no carry
@@ -488,7 +529,6 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
   __syncthreads();
   const uint32_t i = blockIdx.x * SEG + threadIdx.x, seg = blockIdx.x;
   uint32_t lbad = 0, lins = 0;
-  u128 idm = 0;  // the largest id this block's chains insert (exact x_id_max: k_sh_apply folds them)
   if (i < w.E) {
     const uint32_t b = win_batch(w, i);
     const uint32_t first = w.off[b], last = w.off[b + 1] - 1;
@@ -515,7 +555,6 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
         s.ins[j] = commit ? 1 : 0;
         const uint32_t bad = (!commit && j >= e0 && j < e1) ? 1u : 0u;
         const uint32_t ins = (commit && (s.bstatus[j] & ROLE_ID)) ? 1u : 0u;
-        if (XFER && ins) idm = umax128(idm, U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[j].id));
         if (j / SEG == seg) {
           lbad += bad;
           lins += ins;
@@ -527,21 +566,14 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
     }
   }
   const uint32_t wb = wave_sum(lbad), wi = wave_sum(lins);
-  if (XFER) idm = wave_max_u128(idm);
   if ((threadIdx.x & 63) == 0) {
     if (wb) atomicAdd(&nbad, wb);
     if (wi) atomicAdd(&nins, wi);
-    if (XFER) ldsm[threadIdx.x >> 6] = idm;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     if (nbad) atomicAdd(&s.cnt_bad[seg], nbad);
     if (nins) atomicAdd(&s.cnt_ins[seg], nins);
-    if (XFER) {
-      u128 bm = ldsm[0];
-      for (int q = 1; q < SEG / 64; q++) bm = umax128(bm, ldsm[q]);
-      s.blk_idmax[seg] = bm;
-    }
   }
 }
 
@@ -562,11 +594,10 @@ __device__ inline bool sh_abort(const XchView& x, const Globals* g) {
 // are sparse and each inserting lane stores its record whole (no 128 KiB of LDS: twice the resident
 // blocks).
 template <bool XFER, bool STAGE>
-__global__ void __launch_bounds__(SEG) __attribute__((amdgpu_waves_per_eu(STAGE ? 4 : 8))) k_sh_apply(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w, XchView xch,
+__global__ void __launch_bounds__(SEG) __attribute__((amdgpu_waves_per_eu(STAGE ? 4 : SH_APPLY_WPE))) k_sh_apply(Dev d, Scratch s, const uint8_t* ev_bytes, WinDesc w, XchView xch,
                                                   uint32_t hb0, uint32_t hb1, uint32_t e0, uint32_t e1, FinalOut o,
                                                   ChgLog chg, uint32_t chg_epoch) {
   __shared__ uint32_t lds[SEG / 64];
-  __shared__ u128 ldsm[SEG / 64];
   __shared__ uint4 stage[XFER && STAGE ? SEG * 8 : 1];
   Globals* g = d.g;
   // the counters zeroed for the next window (k_sh_decide was their last reader)
@@ -694,21 +725,10 @@ __global__ void __launch_bounds__(SEG) __attribute__((amdgpu_waves_per_eu(STAGE 
   }
   // The last block (by index; the others may still run: they read Globals::base, captured by
   // k_sh_decide, never the counts written here) closes the window from k_sh_decide's per-segment
-  // counts and exact per-segment id maxima.
+  // counts (the id bound was folded by k_sh_decide).
   if (blockIdx.x != gridDim.x - 1) return;
   const uint32_t total_ins = pins + tot_ins;
-  u128 mx = 0;
-  if (XFER) {
-    for (uint32_t j = threadIdx.x; j < gridDim.x; j += SEG) mx = umax128(mx, s.blk_idmax[j]);
-    mx = wave_max_u128(mx);
-    if ((threadIdx.x & 63) == 0) ldsm[threadIdx.x >> 6] = mx;
-    __syncthreads();
-  }
   if (threadIdx.x == 0) {
-    if (XFER) {
-      for (int q = 0; q < SEG / 64; q++) mx = umax128(mx, ldsm[q]);
-      if (mx > g->x_id_max) g->x_id_max = mx;
-    }
     const uint64_t total = xbase + total_ins;
     g->events_total += w.E;
     if (prefix_win) g->x_sorted = total;
