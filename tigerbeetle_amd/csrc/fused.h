@@ -39,6 +39,9 @@
 #define FU_T 256
 #define FU_AMOUNT_MAX (1ull << 43)  // per-event amount bound: 2^20 events x 2^43 <= 2^63
 #define FU_BACKOFF_MAX 8u           // transfer windows the speculation waits at most after a miss
+#ifndef FU_FINAL_GRID
+#define FU_FINAL_GRID 1024u         // k_fu_final's blocks at most (each finishes every FU_FINAL_GRID-th group)
+#endif
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
@@ -444,9 +447,10 @@ __global__ void __launch_bounds__(FU_T) k_ct_fused(Dev d, Scratch s, FuScratch f
 // totals into Globals.
 // fo_only: the general path was not launched for this window (host.inc launch_window); a window
 // outside the class then stops every later window (window_error bit 3) until the host replays them.
+// k: the 256-event group (k_ct_fused's block) of nblk this call finishes.
 __device__ __forceinline__ void fu_final_body(const Dev& d, const Scratch& s, const FuScratch& fs,
                                               const tb_transfer_t* __restrict__ ev, const WinDesc& w, uint32_t epoch,
-                                              const FinalOut& o, uint32_t fo_only) {
+                                              const FinalOut& o, uint32_t fo_only, uint32_t k, uint32_t nblk) {
   __shared__ uint4 stage[FU_T * 4];
   __shared__ uint32_t lds[FU_T / 64];
   __shared__ unsigned long long red[FU_T / 64];
@@ -455,7 +459,7 @@ __device__ __forceinline__ void fu_final_body(const Dev& d, const Scratch& s, co
   Globals* g = d.g;
   // (bit 0 only: this kernel itself may set bit 3, and every block must still undo its adds)
   if ((g->window_error & 1u) || g->fu_epoch != epoch) return;  // (k_ct_fused backed off or skipped)
-  const uint32_t k = blockIdx.x, i = k * FU_T + threadIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t i = k * FU_T + threadIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t E = w.E;
   if (g->fu_abort == epoch) {
     if (k == 0 && threadIdx.x == 0) {
@@ -499,7 +503,7 @@ __device__ __forceinline__ void fu_final_body(const Dev& d, const Scratch& s, co
   }
   __syncthreads();
   const uint32_t total_bad = tb_lds;
-  if (!total_bad && prefix_win && k != gridDim.x - 1 && fs.pnmin[k] == ~0ull) {
+  if (!total_bad && prefix_win && k != nblk - 1 && fs.pnmin[k] == ~0ull) {
     // nothing moves, nothing to index, no expiry entry: only a block where a batch starts has a reply
     // base to write
     const uint32_t lo = k * FU_T, hi = min(E, lo + FU_T), b = win_batch(w, lo);
@@ -579,11 +583,11 @@ __device__ __forceinline__ void fu_final_body(const Dev& d, const Scratch& s, co
       d.exp[*d.exp_cur][g->fu_exp_base + xbase_lds + fs.pbase[k] + rx] = x;
     }
   }
-  if (k == gridDim.x - 1) {
+  if (k == nblk - 1) {
     // the window's totals: the per-block sums folded, the store counts and the window state
     unsigned long long sum = 0, pn = ~0ull;
     u128 mx = 0;
-    for (uint32_t j = threadIdx.x; j < gridDim.x; j += FU_T) {
+    for (uint32_t j = threadIdx.x; j < nblk; j += FU_T) {
       sum += fs.pay[j];
       mx = umax128(mx, fs.idmax[j]);
       pn = fs.pnmin[j] < pn ? fs.pnmin[j] : pn;
@@ -652,7 +656,13 @@ struct ReplyOut {
 template <bool HOST>
 __global__ void __launch_bounds__(FU_T) k_fu_final(Dev d, Scratch s, FuScratch fs, const tb_transfer_t* __restrict__ ev,
                                                    WinDesc w, uint32_t epoch, FinalOut o, uint32_t fo_only, ReplyOut ro) {
-  fu_final_body(d, s, fs, ev, w, epoch, o, fo_only);
+  // a block finishes every gridDim-th group (a clean window's groups mostly exit at once: fewer,
+  // longer-lived blocks than k_ct_fused's grid)
+  const uint32_t nblk = (w.E + FU_T - 1) / FU_T;
+  for (uint32_t k = blockIdx.x; k < nblk; k += gridDim.x) {
+    __syncthreads();  // (the body's LDS words are reused by the next group)
+    fu_final_body(d, s, fs, ev, w, epoch, o, fo_only, k, nblk);
+  }
   if (HOST) {
     __shared__ uint32_t last;
     if (last_block_done(&d.g->fu_done, &last)) {
