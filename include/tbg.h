@@ -141,13 +141,16 @@ int tbg_commit_window_host(tbg_engine *engine, uint32_t operation, const void *h
                            uint32_t *h_batch_base, int auto_pulse, uint64_t prepare_timestamp, uint64_t *ticket);
 /* *done = 1 once window `ticket` finished (h_events reusable, replies written). */
 int tbg_host_window_done(tbg_engine *engine, uint64_t ticket, int *done);
-/* Pinned host memory (hipHostMalloc) for message buffers the engine copies from / to. */
+/* Pinned, device-mapped host memory (hipHostMalloc, mapped) for message buffers the engine reads
+ * from / writes to. */
 int tbg_host_alloc(size_t bytes, void **out);
 int tbg_host_free(void *p);
-/* Page-locks a caller-owned host range in place (hipHostRegister), e.g. a replica's message pool
- * (vsr/message_pool.zig allocates every message buffer once at startup): a tbg_prefetch / tbg_commit
- * request inside a registered or tbg_host_alloc range reaches the device by one DMA, without the copy
- * into the engine's staging buffer. The request must then stay unchanged until its commit returns. */
+/* Page-locks and maps a caller-owned host range in place (hipHostRegister, mapped), e.g. a replica's
+ * message pool (vsr/message_pool.zig allocates every message buffer once at startup): a 16 B-aligned
+ * tbg_prefetch / tbg_commit request inside a registered or tbg_host_alloc range is read by the kernels
+ * in place over PCIe (create_transfers: the fused pass itself, which copies it through to HBM; the
+ * other operations: one copy kernel), without the copy into the engine's staging buffer or a
+ * copy-engine transfer. The request must stay unchanged until its commit returns. */
 int tbg_host_register(void *p, size_t bytes);
 int tbg_host_unregister(void *p);
 
