@@ -247,6 +247,12 @@ enum : uint32_t { SHX_UNSUP = 16 };
 #ifndef SH_APPLY_WPE
 #define SH_APPLY_WPE 8
 #endif
+#ifndef SH_PACK
+#define SH_PACK 1  // k_sh_scan packs an owned-side event's slots and amount for k_sh_apply (G = 8: -6 %)
+#endif
+#ifndef SH_DEC_T
+#define SH_DEC_T 256  // k_sh_decide's block (a divisor of SEG; 1024 measured 1 % slower at G = 8)
+#endif
 
 __device__ inline bool sh_verdict(const XchView& x) { return x.trailer[x.par] != 0; }
 
@@ -299,8 +305,10 @@ __global__ void __launch_bounds__(SH_SCAN_T) __attribute__((amdgpu_waves_per_eu(
   bool owned_id = false;
   uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
   if (i < E) {
-    // per-lane 16 B loads of the record head (staging the wave's heads through LDS, four lanes per
-    // record, measured slower: 51 against 40 us per 1M-event window at G = 8)
+    // per-lane 16 B loads of the record head, all issued together (staging the wave's heads through
+    // LDS, four lanes per record, measured slower: 51 against 40 us per 1M-event window at G = 8; so did
+    // the previous id from the neighbour lane, whose shuffle splits the loads into two round trips, and
+    // the amount loaded only by its owners)
     const uint4* q = reinterpret_cast<const uint4*>(ev_bytes + (size_t)i * 128);
     q0 = q[0];
     if (XFER) {
@@ -385,9 +393,18 @@ __global__ void __launch_bounds__(SH_SCAN_T) __attribute__((amdgpu_waves_per_eu(
     xch.zw[i] = (uint8_t)zw;
     if (XFER) {
       xch.acc[i] = (uint8_t)accb;
+#if SH_PACK
+      // an event with an owned side: its two slots and its amount in one 16 B entry (Scratch::amt),
+      // so k_sh_apply reads one sector instead of two slot sectors and the event row (an amount of
+      // 2^64 or more puts the window outside the class: the low word is the amount)
+      if (roles & (ROLE_DR | ROLE_CR))
+        reinterpret_cast<uint4*>(s.amt)[i] = make_uint4(dslot, cslot, (uint32_t)(uint64_t)amount,
+                                                        (uint32_t)((uint64_t)amount >> 32));
+#else
       // the owned sides' slots only (written and read densely for every event measured slower)
       if (roles & ROLE_DR) s.dr_slot[i] = dslot;
       if (roles & ROLE_CR) s.cr_slot[i] = cslot;
+#endif
     }
     s.bstatus[i] = (uint8_t)roles;
   }
@@ -459,7 +476,7 @@ __device__ inline uint32_t sh_code(const XchView& xch, uint32_t j) {
 }
 
 template <bool XFER>
-__global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes, WinDesc w,
+__global__ void __launch_bounds__(SH_DEC_T) k_sh_decide(Dev d, Scratch s, const uint8_t* __restrict__ ev_bytes, WinDesc w,
                                                    XchView xch, uint32_t e0, uint32_t e1) {
   __shared__ uint32_t nbad, nins;
   Globals* g = d.g;
@@ -468,13 +485,13 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
     // them), whatever the verdict: its blocks' flags and amounts, and every shard's owned inserts
     // against its room (the same capacity verdict on every shard)
     __shared__ uint32_t f_bits, f_cap;
-    __shared__ u128 f_red[SEG / 64], f_mx[SEG / 64];
+    __shared__ u128 f_red[SH_DEC_T / 64], f_mx[SH_DEC_T / 64];
     if (threadIdx.x == 0) f_bits = f_cap = 0;
     __syncthreads();
     const uint32_t nblk = (w.E + SH_SCAN_T - 1) / SH_SCAN_T;
     uint32_t fb = 0;
     u128 fa = 0, fm = 0;
-    for (uint32_t j = threadIdx.x; j < nblk; j += SEG) {
+    for (uint32_t j = threadIdx.x; j < nblk; j += SH_DEC_T) {
       fb |= s.blk_aux[j];
       if (XFER) {
         fa += s.blk_amt[j];
@@ -483,7 +500,7 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
     }
     if (fb) atomicOr(&f_bits, fb);
     // shard g's owned-id slots: wave g, one slot per lane
-    for (uint32_t sg = threadIdx.x >> 6; sg < xch.G; sg += SEG / 64) {
+    for (uint32_t sg = threadIdx.x >> 6; sg < xch.G; sg += SH_DEC_T / 64) {
       const uint32_t tot = wave_sum(xch.own[sg * SH_OWN_SLOTS + (threadIdx.x & 63)]);
       if ((threadIdx.x & 63) == 0 && tot > xch.room[sg]) atomicOr(&f_cap, 1u);
     }
@@ -504,7 +521,7 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
       g->sh_cap_bad = f_cap;
       if (XFER) {
         u128 amt = 0, mx = 0;
-        for (int q = 0; q < SEG / 64; q++) {
+        for (int q = 0; q < SH_DEC_T / 64; q++) {
           amt += f_red[q];
           mx = umax128(mx, f_mx[q]);
         }
@@ -527,7 +544,7 @@ __global__ void __launch_bounds__(SEG) k_sh_decide(Dev d, Scratch s, const uint8
   if (sh_verdict(xch)) return;  // outside the class: k_sh_apply reports it
   if (threadIdx.x == 0) nbad = nins = 0;
   __syncthreads();
-  const uint32_t i = blockIdx.x * SEG + threadIdx.x, seg = blockIdx.x;
+  const uint32_t i = blockIdx.x * SH_DEC_T + threadIdx.x, seg = i / SEG;  // (blocks of one segment share its counters)
   uint32_t lbad = 0, lins = 0;
   if (i < w.E) {
     const uint32_t b = win_batch(w, i);
@@ -651,14 +668,24 @@ __global__ void __launch_bounds__(SEG) __attribute__((amdgpu_waves_per_eu(STAGE 
   const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rins, 0);  // the wave's first insert rank
   if (commit) {
     if (XFER) {
+#if SH_PACK
+      uint4 pk = make_uint4(NONE32, NONE32, 0, 0);
+      if (roles & (ROLE_DR | ROLE_CR)) pk = reinterpret_cast<const uint4*>(s.amt)[i];
+      uint32_t drs = (roles & ROLE_DR) ? pk.x : NONE32, crs = (roles & ROLE_CR) ? pk.y : NONE32;
+#else
       uint32_t drs = (roles & ROLE_DR) ? s.dr_slot[i] : NONE32, crs = (roles & ROLE_CR) ? s.cr_slot[i] : NONE32;
+#endif
       if (drs != NONE32 && !sh_guard(g, drs < d.acc_max, 3, drs)) drs = NONE32;
       if (crs != NONE32 && !sh_guard(g, crs < d.acc_max, 4, crs)) crs = NONE32;
       if (ins && !sh_guard(g, xbase + rins < d.x_max, 5, xbase + rins)) ins = false;
       const tb_transfer_t* t = reinterpret_cast<const tb_transfer_t*>(ev_bytes) + i;
       Add128 a_dr, a_cr;
       if (drs != NONE32 || crs != NONE32) {
+#if SH_PACK
+        const u128 a = ((uint64_t)pk.w << 32) | pk.z;
+#else
         const u128 a = U(t->amount);
+#endif
         if (drs != NONE32) a_dr.issue(&d.acc[drs].debits_posted, a, small);
         if (crs != NONE32) a_cr.issue(&d.acc[crs].credits_posted, a, small);
         if (chg.mark) {  // write-back stream (changes.h): the owned accounts this window changed
