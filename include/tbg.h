@@ -162,6 +162,10 @@ int tbg_sync(tbg_engine *engine);
 int tbg_windows_committed(tbg_engine *engine, uint64_t *applied, uint64_t *submitted);
 /* The engine's HIP stream (hipStream_t), for callers that time or order around it. */
 void *tbg_stream(tbg_engine *engine);
+/* Copies n bytes of device memory to `host` after the work queued on the engine stream, and waits:
+ * a kernel on the stream writes them through the engine's mapped pinned block, so no copy-engine
+ * handoff (~10 us each side) is paid on a small read (replies, counts). Any n, any alignment. */
+int tbg_read_device(tbg_engine *engine, void *host, const void *d_src, uint64_t n);
 
 /* Hash-sharded commit over G GPUs of one node (tigerbeetle_amd/csrc/shard.h). The replacement for
  * the same commit (state_machine.zig:1220-1306) when accounts are partitioned across engines:

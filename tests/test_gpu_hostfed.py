@@ -141,3 +141,27 @@ def test_host_fed_done_is_per_ticket():
     finally:
         gpu.close()
         ref.close()
+
+
+@pytest.mark.gpu
+def test_read_device_any_size_and_alignment():
+    """tbg_read_device: a kernel copy through the engine's pinned block, after the stream's work; any
+    byte count (beyond one pinned block too) and any alignment of the device source."""
+    import torch
+
+    from tigerbeetle_amd import StateMachine
+
+    sm = StateMachine(batch_max=64, accounts_max=1024, transfers_max=1024)
+    try:
+        g = torch.Generator().manual_seed(5)
+        src = torch.randint(0, 256, (3 * 64 * 128 + 77,), dtype=torch.uint8, generator=g)
+        d = src.cuda()
+        torch.cuda.synchronize()
+        for off, n in [(0, 0), (0, 1), (3, 17), (16, 4096), (5, 64 * 128 + 3), (1, 3 * 64 * 128 + 70)]:
+            got = sm.read_device(d[off: off + n])
+            assert np.array_equal(got, src[off: off + n].numpy()), (off, n)
+        w = torch.arange(1000, dtype=torch.int32).cuda()
+        torch.cuda.synchronize()
+        assert np.array_equal(sm.read_device(w), np.arange(1000, dtype=np.int32))
+    finally:
+        sm.close()

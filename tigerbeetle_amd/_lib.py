@@ -11,7 +11,7 @@ LIB_PATH = os.path.join(HERE, "libtbgpu.so")
 # Every symbol declared in include/tbg.h.
 EXPORTS = [
     "tbg_create", "tbg_destroy", "tbg_input_valid", "tbg_pulse_needed", "tbg_prefetch", "tbg_commit",
-    "tbg_commit_device", "tbg_commit_window", "tbg_sync", "tbg_stream", "tbg_setup_balances", "tbg_get_stats",
+    "tbg_commit_device", "tbg_commit_window", "tbg_sync", "tbg_read_device", "tbg_stream", "tbg_setup_balances", "tbg_get_stats",
     "tbg_dump_accounts", "tbg_dump_transfers", "tbg_dump_transfer_status", "tbg_device_stores",
     "tbg_gen_accounts", "tbg_gen_transfers_uniform", "tbg_gen_permute_ids", "tbg_gen_mark_pending", "tbg_version", "tbg_debug_last_batch",
     "tbg_timing_enable", "tbg_timing_collect", "tbg_gen_accounts_cfg3", "tbg_gen_funding_cfg3",
@@ -106,6 +106,7 @@ def lib():
         "tbg_commit_device": ([vp, u32, u64, vp, u32, vp, vp, ctypes.c_int, u64], i32),
         "tbg_commit_window": ([vp, u32, vp, u32, vp, vp, vp, vp, ctypes.c_int, u64], i32),
         "tbg_sync": ([vp], i32),
+        "tbg_read_device": ([vp, vp, vp, u64], i32),
         "tbg_stream": ([vp], vp),
         "tbg_setup_balances": ([vp, P(U128), P(U128), P(U128), P(U128), P(U128)], i32),
         "tbg_get_stats": ([vp, P(Stats)], i32),

@@ -1662,6 +1662,13 @@ __global__ void k_clear_bits(uint32_t* p, uint32_t bits) { atomicAnd(p, ~bits); 
 __global__ void __launch_bounds__(256) k_copy_in(uint4* __restrict__ dst, const uint4* __restrict__ src, uint32_t n16) {
   for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n16; k += gridDim.x * 256) dst[k] = src[k];
 }
+// Any bytes (tbg_read_device): 16-byte words when both sides are aligned, then the tail.
+__global__ void __launch_bounds__(256) k_copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n) {
+  const uint32_t n16 = ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) ? n / 16 : 0u;
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n16; k += gridDim.x * 256)
+    reinterpret_cast<uint4*>(dst)[k] = reinterpret_cast<const uint4*>(src)[k];
+  for (uint32_t k = n16 * 16 + blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) dst[k] = src[k];
+}
 // The Globals ([0, g16) words) and, with the reply, the reply block at H_REPLY_OFF (its count and the
 // first min(count, n_max) results): the same layout on both sides. flag (one block only): written
 // with `seq` after every word, for the host to poll (reply_flag_out).

@@ -361,7 +361,7 @@ class ShardedStateMachine:
         from .state_machine import to_host
 
         with _timed(self, 1):
-            c = to_host(self.gw_cnt).view(np.uint32).reshape(self.shard_count, 4)
+            c = self.sm.read_device(self.gw_cnt).view(np.uint32).reshape(self.shard_count, 4)
         if (c[:, 3] > self.due_cap).any():
             self.gw_fallbacks["due_overflow"] += 1
             self.invalidate_scratch()
@@ -418,8 +418,8 @@ class ShardedStateMachine:
             self.invalidate_scratch()  # (its first pulse may have run in the scratch: it starts over)
             return None
         self.gw_acc_base = held.value
-        base = to_host(self.gw_base)
-        res = to_host(self.gw_res[: int(base[nb]) * 8]).tobytes()
+        base = self.sm.read_device(self.gw_base)
+        res = self.sm.read_device(self.gw_res[: int(base[nb]) * 8]).tobytes()
         return [res[base[b] * 8: base[b + 1] * 8] for b in range(nb)]
 
     def commit_general_window(self, operation, d_events, batch_events, batch_timestamps, auto_pulse=True):
@@ -499,8 +499,8 @@ class ShardedStateMachine:
             sc.commit_window(operation, d_events, [n], [timestamp], self.gx_res.data_ptr(), self.gx_base.data_ptr(),
                              auto_pulse, timestamp)
             sc.sync()
-            base = to_host(self.gx_base)
-            reply = to_host(self.gx_res[: int(base[1]) * 8]).tobytes()
+            base = self.sm.read_device(self.gx_base)
+            reply = self.sm.read_device(self.gx_res[: int(base[1]) * 8]).tobytes()
         pa, na, px, ps, nx, pn2 = (ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_void_p(),
                                    ctypes.c_uint64(), ctypes.c_uint64())
         _lib.check(L.tbg_device_state(sc.h, ctypes.byref(pa), ctypes.byref(na), ctypes.byref(px), ctypes.byref(ps),

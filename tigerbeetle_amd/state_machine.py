@@ -27,6 +27,13 @@ def to_host(t):
     return c.numpy().copy()
 
 
+def _np_dtype(dt):
+    import torch
+
+    return {torch.uint8: np.uint8, torch.int32: np.int32, torch.int64: np.int64, torch.uint32: np.uint32,
+            torch.float32: np.float32}[dt]
+
+
 class HostBuffer:
     """Pinned host memory from tbg_host_alloc, as a uint8 array: a replica's message buffer (allocated
     once, vsr/message_pool.zig). A request in it reaches the device by one DMA (include/tbg.h
@@ -207,6 +214,13 @@ class StateMachine:
 
     def sync(self):
         _lib.check(_lib.lib().tbg_sync(self.h), "sync")
+
+    def read_device(self, t):
+        """A device tensor (contiguous) as a numpy array, after the work queued on the engine stream:
+        a kernel copy through the engine's pinned block (tbg_read_device), no copy-engine handoff."""
+        out = np.empty(t.numel() * t.element_size(), dtype=np.uint8)
+        _lib.check(_lib.lib().tbg_read_device(self.h, out.ctypes.data, t.data_ptr(), out.nbytes), "read_device")
+        return out.view(_np_dtype(t.dtype)).reshape(tuple(t.shape))
 
     # ---- the rest of the reference surface the replica drives ------------------------------
     def open(self, accounts, transfers, pending_status, account_balances=None):
