@@ -1365,16 +1365,25 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
     }
   }
   if (XFER) {
+    // the block's entries from ONE counter atomic: one per wave on the same word serialized at the
+    // memory side (a cfg4 window appends from almost every wave)
+    __shared__ uint32_t xw[SEG / 64];
+    __shared__ unsigned long long xq;
     const unsigned long long m = __ballot(xapp);
-    if (m) {
-      const int leader = __builtin_ctzll(m);
-      unsigned long long q = 0;
-      if ((int)lane == leader)
-        q = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), (unsigned long long)__popcll(m));
-      q = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(q >> 32), leader) << 32) |
-          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q, leader);
-      if (xapp) d.exp[*d.exp_cur][q + (unsigned long long)__popcll(m & ((1ull << lane) - 1))] = xent;
+    const uint32_t wave = threadIdx.x >> 6;
+    if (lane == 0) xw[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SEG / 64; k++) {
+      const uint32_t v = xw[k];
+      before += k < wave ? v : 0u;
+      tot += v;
     }
+    if (threadIdx.x == 0 && tot)
+      xq = atomicAdd(reinterpret_cast<unsigned long long*>(&d.g->exp_count), (unsigned long long)tot);
+    __syncthreads();
+    if (xapp) d.exp[*d.exp_cur][xq + before + (unsigned long long)__popcll(m & ((1ull << lane) - 1))] = xent;
   }
   // Compact this wave's inserted records in LDS, then store them as one contiguous run (a wave
   // with only in-place records stores nothing).
