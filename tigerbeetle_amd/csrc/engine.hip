@@ -1479,7 +1479,7 @@ __device__ inline bool window_spans_pulse(const WinChk& c, uint64_t pulse_next) 
 // every window after it change nothing until tbg_sync reports it; the scan only read the live list,
 // so a rejected pulse leaves everything as it was. cand_count, alt_count and next_min are zero on
 // entry (the tail leaves them so).
-#define PULSE_BLOCKS 16  // few blocks: each pays an agent-scope fence before the last one runs the tail
+#define PULSE_BLOCKS 64  // few blocks: each pays an agent-scope fence before the last one runs the tail
 __global__ void __launch_bounds__(1024) k_pulse(Dev d, Scratch s, uint64_t T, uint64_t prepare_timestamp,
                                                uint32_t cap, ChgLog chg, uint32_t chg_epoch, WinChk chk) {
   __shared__ uint32_t hist[256];
@@ -1498,27 +1498,48 @@ __global__ void __launch_bounds__(1024) k_pulse(Dev d, Scratch s, uint64_t T, ui
   const ExpEntry* list = d.exp[cur];
   ExpEntry* alt = d.exp[cur ^ 1];
   const uint64_t count = g->exp_count;
-  // (appends aggregated per wave, the minimum per wave: same-address atomics serialize)
-  const uint32_t lane = threadIdx.x & 63;
+  // (appends aggregated per block and pass, the minimum per wave: same-address atomics serialize)
+  __shared__ uint32_t wd[1024 / 64], wl[1024 / 64];
+  __shared__ uint32_t bd, bl;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const unsigned long long lt = (1ull << lane) - 1;
   unsigned long long nmin = ~0ull;
-  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < count; j += (uint64_t)gridDim.x * blockDim.x) {
-    const ExpEntry e = list[j];
-    const bool live = d.xstatus[e.slot] == TB_PENDING_PENDING;  // else removed from the index
+  for (uint64_t j0 = blockIdx.x * (uint64_t)blockDim.x; j0 < count; j0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t j = j0 + threadIdx.x;  // (block-uniform trip count: the barriers below)
+    ExpEntry e{};
+    bool live = false;
+    if (j < count) {
+      e = list[j];
+      live = d.xstatus[e.slot] == TB_PENDING_PENDING;  // else removed from the index
+    }
     const bool due = live && e.expires_at <= T;
     const bool later = live && !due;
     const unsigned long long md = __ballot(due), ml = __ballot(later);
-    const int ld = md ? __builtin_ctzll(md) : 0, ll = ml ? __builtin_ctzll(ml) : 0;
-    uint32_t bd = 0, bl = 0;
-    if (md && (int)lane == ld) bd = atomicAdd(&g->cand_count, (uint32_t)__popcll(md));
-    if (ml && (int)lane == ll) bl = atomicAdd(&g->alt_count, (uint32_t)__popcll(ml));
-    bd = __shfl(bd, ld, 64);
-    bl = __shfl(bl, ll, 64);
-    if (due) s.cand[bd + (uint32_t)__popcll(md & lt)] = e;
+    if (lane == 0) {
+      wd[wave] = (uint32_t)__popcll(md);
+      wl[wave] = (uint32_t)__popcll(ml);
+    }
+    __syncthreads();
+    uint32_t pd = 0, pl = 0, td = 0, tl = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 1024 / 64; k++) {
+      const uint32_t vd = wd[k], vl = wl[k];
+      pd += k < wave ? vd : 0u;
+      pl += k < wave ? vl : 0u;
+      td += vd;
+      tl += vl;
+    }
+    if (threadIdx.x == 0) {
+      bd = td ? atomicAdd(&g->cand_count, td) : 0u;
+      bl = tl ? atomicAdd(&g->alt_count, tl) : 0u;
+    }
+    __syncthreads();
+    if (due) s.cand[bd + pd + (uint32_t)__popcll(md & lt)] = e;
     if (later) {
-      alt[bl + (uint32_t)__popcll(ml & lt)] = e;
+      alt[bl + pl + (uint32_t)__popcll(ml & lt)] = e;
       nmin = umin64(nmin, e.expires_at);
     }
+    __syncthreads();  // (wd, wl, bd, bl: the next pass)
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) nmin = umin64(nmin, (unsigned long long)__shfl_xor(nmin, o, 64));
