@@ -57,6 +57,7 @@ __global__ void k_xwin_decide(Dev d, Scratch s, WinDesc w, uint32_t cap) {
   bool bad = g->hot_count != 0 || g->batch_huge || ovf128(g->ovf_bound, g->batch_amount_sum) || (g->win_flags & 16u);
   // (a pulse that fills its buffer, cap entries or more, ends buffer_finished: not modelled)
   for (uint32_t b = 1; b < w.nb; b++) bad = bad || s.xw_cnt[b] >= cap;
+  for (uint32_t b = 0; b < MAXB; b++) s.xw_cnt[b] = 0;  // (zero again for the next window's count)
   if (!bad) return;
   atomicOr(&g->window_error, 1u);
   g->hot_count = 0;
@@ -69,6 +70,9 @@ __global__ void k_xwin_decide(Dev d, Scratch s, WinDesc w, uint32_t cap) {
 // Removal batch of each pending transfer the window created (committed post/voids of it).
 __global__ void __launch_bounds__(256) k_xwin_rb(Dev d, Scratch s, WinDesc w) {
   if (WIN_REJECTED(d.g)) return;
+  // k_xwin_minlive's minima start at "none" (xw_tree, xw_minx, xw_miny: one allocation)
+  if (blockIdx.x == 0)
+    for (uint32_t j = threadIdx.x; j < 4 * MAXB; j += blockDim.x) s.xw_tree[j] = ~0ull;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < w.E; k += gridDim.x * blockDim.x) {
     const uint32_t cls = s.cls[k];
     if ((cls & C_POSTVOID) && (cls & C_PNOP) && s.code[k] == TB_CT_OK && s.p_tslot[k] == NONE32)
