@@ -317,8 +317,10 @@ class ShardedStateMachine:
         sc = self.wscratch
         if sc is not None and self.gw_acc_cap >= acc_need and self.gw_x_cap >= x_need and self.gw_sc_events >= n_events:
             return
-        acc_cap = max(int(acc_need * 1.25) + 1024, getattr(self, "gw_acc_cap", 0))
-        x_cap = max(int(x_need * 1.25) + 1024, getattr(self, "gw_x_cap", 0))
+        # (accounts doubling: a stream whose read set grows window by window re-creates the scratch
+        # engine, and restarts it with a full reload, a logarithmic number of times)
+        acc_cap = max(2 * acc_need + 1024, 2 * getattr(self, "gw_acc_cap", 0) if sc is not None else 0)
+        x_cap = max(int(x_need * 1.25) + 1024, getattr(self, "gw_x_cap", 0))  # (its table is reset per window)
         ev_cap = max(n_events, getattr(self, "gw_sc_events", 0))
         if sc is not None:
             sc.close()
