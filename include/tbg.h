@@ -397,6 +397,9 @@ typedef struct tbg_stats {
 int tbg_get_stats(tbg_engine *engine, tbg_stats *out);
 
 /* Debug: cumulative resolver counters (see host.inc); up to 8 values. */
+/* Debug: entries in use of the account and transfer hash tables (every window in flight settled).
+ * Bounded by the stored accounts / hashed transfers: an aborted fused window leaves no entry behind. */
+int tbg_debug_table_used(tbg_engine *engine, uint64_t *accounts_used, uint64_t *transfers_used);
 int tbg_debug_counters(tbg_engine *engine, uint64_t *out, uint32_t n);
 
 /* Write-back stream of the last commit call (TBG_FLAG_CHANGE_LOG; state_machine.zig groove side

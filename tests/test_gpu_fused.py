@@ -694,3 +694,47 @@ def test_fused_pending_creates_in_class(order):
     finally:
         gpu.close()
         ref.close()
+
+
+@pytest.mark.gpu
+def test_fused_claim_mode_aborts_leave_the_table_bounded():
+    """Claim mode (random ids) with every window leaving the class after its claims were made (a chain
+    in its last batch, a post of a stored pending transfer in another): the claims are reverted to the
+    empty entries they took, so after every window the transfer table holds exactly one entry per
+    hashed record (no removed entries accumulate: ADVICE r5, a table with no empty entry left would
+    make every probe loop), and replies and stores equal the restatement's."""
+    from tigerbeetle_amd import _lib
+    import ctypes
+
+    n_acc = 2000
+    gpu, ref = _engines(n_acc, 1 << 17)
+    code = workload.ID_ORDERS["random"]
+    L = _lib.lib()
+
+    def used():
+        a, x = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(L.tbg_debug_table_used(gpu.h, ctypes.byref(a), ctypes.byref(x)), "table_used")
+        return a.value, x.value
+
+    try:
+        _accounts(gpu, ref, n_acc)
+        first = 0
+        for w in range(10):
+            b = _window(first, n_acc, seed=61 + w)
+            first += WIN * BM
+            flat = np.concatenate(b)
+            ids = workload.permute_ids(flat.copy(), code, 5)
+            flat["id_lo"], flat["id_hi"] = ids["id_lo"], ids["id_hi"]
+            b = [flat[k * BM:(k + 1) * BM].copy() for k in range(WIN)]
+            if w % 3 != 2:  # (every third window stays in the class: the speculation re-arms)
+                b[WIN - 1]["flags"][BM - 10] = 1  # linked: a chain of two, in the last block
+            _check(gpu, ref, b)
+            st = gpu.stats()
+            acc_used, x_used = used()
+            assert acc_used == st["accounts"], (w, acc_used, st)
+            assert x_used == st["transfers"] - st["sorted_transfers"], (w, x_used, st)
+        assert gpu.stats()["fused_windows"] >= 2
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()

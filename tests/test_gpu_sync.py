@@ -109,3 +109,46 @@ def test_sync_registered_caller_buffer_and_unregistered_fallback():
             g.close()
         ref.close()
         _lib.check(L.tbg_host_unregister(ctypes.c_void_p(buf.ctypes.data)), "host_unregister")
+
+
+@pytest.mark.gpu
+def test_sync_state_reads_between_prefetch_and_commit():
+    """A replica may read state between a prefetch and its commit (pulse() after open/reset, stats,
+    tbg_sync, tbg_read_device: replica.zig:3134's pulse_timeout path). With a request in pageable memory
+    (staged by the engine), none of those reads may touch the staged request (they used to
+    land in the same pinned block): replies, pulse() decisions and stores equal the restatement's."""
+    import torch
+
+    from tigerbeetle_amd import StateMachine
+
+    gpu = StateMachine(batch_max=BM, accounts_max=1024, transfers_max=1 << 15)
+    ref = OracleStateMachine(batch_max=BM)
+    probe = torch.arange(4096, dtype=torch.uint8, device="cuda")
+    try:
+        for k, (op, ev, tick) in enumerate(_stream(21, 30)):
+            raw = ev.tobytes()
+            for sm in (gpu, ref):
+                sm.prepare_timestamp += tick + 1
+                sm.prepare(op, raw)
+            T = gpu.prepare_timestamp
+            p1, p2 = gpu.pulse(), ref.pulse()
+            assert p1 == p2, k
+            for sm in (gpu, ref):
+                if p1:
+                    sm.prefetch_timestamp = T
+                    sm.prefetch(1, Operation.pulse, b"")
+                    sm.commit(0, 1, T, Operation.pulse, b"")
+                sm.prefetch_timestamp = T
+                sm.prefetch(2, op, raw)
+            # state reads between the prefetch and the commit (GPU side)
+            gpu.stats()
+            gpu.sync()
+            assert gpu.pulse() == ref.pulse(), k
+            assert gpu.read_device(probe)[:8].tolist() == list(range(8))
+            r1 = gpu.commit(0, 2, T, op, raw)
+            r2 = ref.commit(0, 2, T, op, raw)
+            assert r1 == r2, k
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()

@@ -25,6 +25,7 @@ EXPORTS = [
     "tbg_gw_collect", "tbg_gw_write", "tbg_gw_commit", "tbg_gw_result",
     "tbg_shard_apply", "tbg_open_device", "tbg_device_state", "tbg_device_history", "tbg_shard_lookup_bytes",
     "tbg_shard_lookup", "tbg_shard_lookup_reply", "tbg_shard_query_bytes", "tbg_shard_query", "tbg_shard_query_merge",
+    "tbg_debug_table_used",
 ]
 
 
@@ -127,6 +128,7 @@ def lib():
         "tbg_gen_transfers_zipf": ([vp, u64, u64, u64, u64, vp, u64, vp], i32),
         "tbg_gen_transfers_cfg4": ([vp, u64, u64, u64, u64, u64, u64, vp], i32),
         "tbg_debug_counters": ([vp, vp, u32], i32),
+        "tbg_debug_table_used": ([vp, P(u64), P(u64)], i32),
         "tbg_shard_of": ([u64, u64, u32], u32),
         "tbg_shard_prepare_window": ([vp, u32, vp, u32, vp, vp, vp], i32),
         "tbg_shard_commit_window": ([vp, vp, u32, u32, vp, vp], i32),

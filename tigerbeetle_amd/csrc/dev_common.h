@@ -38,7 +38,6 @@ static_assert(sizeof(AccEntry) == 32, "AccEntry");
 
 typedef unsigned long long XEntry;  // [63:32] high half of the id hash, [31:0] record slot
 #define X_EMPTY 0xFFFFFFFFFFFFFFFFull  // slot NONE32 never occurs in a live entry
-#define X_TOMB 0xFFFFFFFFFFFFFFFEull   // a removed entry (the fused pass's claims, fused.h): probed past, never matched
 
 // Window-local key map. Entries are epoch-tagged (the window number), so a stale entry from an
 // earlier window reads as empty and nothing is ever reset. Keys are never stored: `key` names the
@@ -272,16 +271,13 @@ __device__ inline uint32_t acc_find(const AccEntry* __restrict__ tab, uint64_t m
 }
 
 // Continues a transfer-id probe whose first entry `e` (at h & mask) is already loaded.
-// slot_lim: entries at or past it are passed over (the fused pass's undo: the claims of the window
-// being undone, fused.h).
 __device__ inline uint32_t x_probe_from(const XEntry* __restrict__ tab, const tb_transfer_t* __restrict__ xr,
-                                        uint64_t mask, uint64_t h, XEntry e, tb_uint128_t id,
-                                        uint64_t slot_lim = ~0ull) {
+                                        uint64_t mask, uint64_t h, XEntry e, tb_uint128_t id) {
   const uint32_t fp = (uint32_t)(h >> 32);
   uint64_t pos = h & mask;
   for (;;) {
     if (e == X_EMPTY) return NONE32;
-    if ((uint32_t)(e >> 32) == fp && e != X_TOMB && (uint32_t)e < slot_lim) {
+    if ((uint32_t)(e >> 32) == fp) {
       const tb_uint128_t k = xr[(uint32_t)e].id;
       if (k.lo == id.lo && k.hi == id.hi) return (uint32_t)e;
     }
@@ -397,7 +393,7 @@ __device__ inline uint32_t x_probe_claim(XEntry* tab, const tb_transfer_t* __res
       e = seen;  // another claim took it first: examine that one
       continue;
     }
-    if (e != X_TOMB && (uint32_t)(e >> 32) == fp) {
+    if ((uint32_t)(e >> 32) == fp) {
       const uint32_t slot = (uint32_t)e;
       if (slot < base) {
         const tb_uint128_t k = xr[slot].id;

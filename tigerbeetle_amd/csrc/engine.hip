@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstddef>
 #include <new>
 #include <vector>
@@ -1717,6 +1718,22 @@ __global__ void __launch_bounds__(256) k_reply_out(const uint4* __restrict__ dev
     host[j] = dev[j];
   }
   if (flag) reply_flag_out(flag, seq);
+}
+
+// Entries in use of the two hash tables (tbg_debug_table_used): out[0] accounts, out[1] transfers.
+__global__ void __launch_bounds__(256) k_table_used(Dev d, unsigned long long* out) {
+  unsigned long long na = 0, nx = 0;
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k <= d.x_mask || k <= d.acc_mask;
+       k += (uint64_t)gridDim.x * 256) {
+    if (k <= d.acc_mask && d.acc_tab[k].slot != NONE32) na++;
+    if (k <= d.x_mask && d.x_tab[k] != X_EMPTY) nx++;
+  }
+  na = wave_sum_u64(na);
+  nx = wave_sum_u64(nx);
+  if ((threadIdx.x & 63) == 0) {
+    if (na) atomicAdd(out, na);
+    if (nx) atomicAdd(out + 1, nx);
+  }
 }
 
 // Harness `setup` (state_machine.zig:2545-2561).

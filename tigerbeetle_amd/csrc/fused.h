@@ -28,8 +28,8 @@
 //
 // Speculation. Each block applies its balance adds as soon as its own events are simple; whether the
 // whole window is simple is known after the launch (Globals::fu_abort = this window's epoch when a
-// block was not). If it is not, k_fu_final subtracts the adds of every block that applied (recomputing
-// the same decisions from the same unchanged inputs: nothing the decisions read is written here), and
+// block was not). If it is not, k_fu_final subtracts the adds of every block that applied (its ok
+// events, from the per-wave bitmap the applying blocks wrote; the accounts probed again), and
 // the general path runs the window as if this pass had not (its record and status stores are all
 // rewritten or beyond the store's end). Globals::sp_done tells the general path's kernels to return
 // at once when the fused pass committed the window. A window that is not simple backs the speculation
@@ -75,15 +75,15 @@ struct FuEv {
 // duplicate (another event's claim: outside the class) and indexes the new record. k_fu_final re-points
 // the claims of records that move down to their ranks (by the claim's position, fs.cpos: never by a
 // search, which could meet another record's re-pointed entry), and removes every claim of a window
-// that leaves the class. (Round 4 claimed in the window key map and inserted into the table after the
+// that leaves the class (reverted to the empty entries they took: the table is restored exactly). (Round 4 claimed in the window key map and inserted into the table after the
 // window: two random probe sequences per event.)
 
 // prev_id: the id of event i - 1 (i > 0). ts: the event's timestamp (the record as inserted). base:
 // the window's first record slot. claim: claim mode (ev: the window's events, E of them), else the
-// ids must rise. undo (k_fu_final): the same decision again, the window's own claims passed over.
+// ids must rise.
 __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id, const tb_transfer_t& t, uint64_t ts,
                                           u128 x_id_max, uint64_t P, uint64_t base, FuEv* o, bool claim = false,
-                                          const tb_transfer_t* ev = nullptr, uint32_t E = 0, bool undo = false) {
+                                          const tb_transfer_t* ev = nullptr, uint32_t E = 0) {
   const uint16_t f = t.flags;
   o->dr = o->cr = NONE32;
   o->amount = 0;
@@ -147,7 +147,7 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
                 xs = x_probe_claim(d.x_tab, d.xr, ev, d.x_mask, hx, ex, t.id, base, i, E, !tovf, &dup, &o->cpos);
               if (dup) simple = false;  // in-window duplicate
             } else {
-              xs = mx ? x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id, undo ? base : ~0ull) : NONE32;
+              xs = mx ? x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id) : NONE32;
               if (xs == NONE32 && mx) xs = x_prefix_find(d.xr, P, t.id);
             }
             // :1506-1507
@@ -475,22 +475,27 @@ __device__ __forceinline__ void fu_final_body(const Dev& d, const Scratch& s, co
       }
     }
     if (i >= E) return;
-    // claim mode: every claim of the window removed (blocks that applied or not), before the general
-    // path sees the table
+    // claim mode: every claim of the window reverted to the empty entry it took (blocks that applied or
+    // not). The window's claims are the only writes the table had since the previous window, and
+    // nothing here probes the table (the undo below reads the ok bitmap), so reverting all of them
+    // restores the table exactly: no tombstones accumulate over aborted windows.
     if (g->fu_claim) {
       const uint32_t p = fs.cpos[i];
-      if (p != NONE32) d.x_tab[p] = X_TOMB;
+      if (p != NONE32) d.x_tab[p] = X_EMPTY;
     }
     if (!fs.applied[k]) return;
+    // the adds this block applied: its ok events (k_ct_fused's per-wave bitmap, written by every
+    // applying block), each to its two accounts' posted or pending fields
+    if (!((fs.ok[i >> 6] >> lane) & 1ull)) return;
+    const tb_transfer_t& t = ev[i];
+    AccEntry ae;
     FuEv fe;
-    // (no claims: the undo needs the codes, amounts, fields and accounts only; the window's own claims
-    // are passed over, so each event finds what it found before)
-    fu_decide(d, i, i > 0 ? U(ev[i - 1].id) : (u128)0, ev[i], win_ts(w, win_batch(w, i), i), g->x_id_max,
-              g->x_sorted, g->fu_base, &fe, false, nullptr, 0, true);
-    if (fe.code == TB_CT_OK) {
-      (void)atomicAdd(fu_dr_field(d, fe), 0ull - fe.amount);
-      (void)atomicAdd(fu_cr_field(d, fe), 0ull - fe.amount);
-    }
+    fe.pending = (t.flags & TB_TRANSFER_PENDING) != 0;
+    fe.dr = acc_find(d.acc_tab, d.acc_mask, t.debit_account_id, &ae);
+    fe.cr = acc_find(d.acc_tab, d.acc_mask, t.credit_account_id, &ae);
+    if (fe.dr == NONE32 || fe.cr == NONE32) return;  // (never: an ok event found both)
+    (void)atomicAdd(fu_dr_field(d, fe), 0ull - t.amount.lo);
+    (void)atomicAdd(fu_cr_field(d, fe), 0ull - t.amount.lo);
     return;
   }
   const uint64_t base = g->fu_base;
