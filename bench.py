@@ -84,7 +84,7 @@ CONFIGS = {
     "cfg3": dict(accounts=1_000_000, transfers=10_000_000, window=32, seed=45, tick=0),
     "cfg4": dict(accounts=1_000_000, transfers=10_000_000, window=128, seed=46, tick=NS_PER_S),
     # per GPU (weak scaling): 100M accounts / 1B transfers at 8 GPUs
-    "cfg5": dict(accounts=12_500_000, transfers=125_000_000, window=64, seed=47, tick=0),
+    "cfg5": dict(accounts=12_500_000, transfers=125_000_000, window=128, seed=47, tick=0),
 }
 PENDING_TIMEOUT = 3600  # --pending-every: pending creates that stay pending for the whole run
 CFG3_TREASURY, CFG3_TOP, CFG3_FUND, CFG3_FUND_ID = 1000, 1000, 1_000_000, 10**15
@@ -123,7 +123,7 @@ def pmc_traffic(config, kernel, events_per_launch):
     scaled to this run's events per launch. None when this line has no summary of its own (a
     variant's traffic is never borrowed from another line's). Returns (raw FETCH+WRITE bytes, bytes
     with FETCH doubled per the gfx950 streaming-read correction, source) or None."""
-    for rnd in ("r5", "r4", "r3", "r2", "r1"):  # the latest round's summary of this config
+    for rnd in ("r6", "r5", "r4", "r3", "r2", "r1"):  # the latest round's summary of this config
         path = os.path.join(ROOT, "profiles", rnd, "pmc_%s.json" % config)
         if os.path.exists(path):
             break
@@ -417,127 +417,153 @@ def _cpu_baseline(args, seed):
     return line
 
 
-# Algorithmic bytes per event of the sharded kernels on one of G shards: every shard
-# reads each event's ids and writes its facts; owned probes / effects are 1/G each.
-def shard_kernel_bytes(kernel, G, prefix):
-    """Algorithmic bytes per window event of the sharded scan / apply kernels (csrc/shard.h)."""
-    if kernel == "prep":
-        # k_sh_scan, per window event: the ids (64) read by every shard, the 2 B of facts and the roles
-        # byte written; the id owner (1/G) reads the rest of the event (64) and, with monotonic fresh ids,
-        # probes nothing; the account owners (2/G) probe one 32 B table entry and store a 4 B slot
-        return 64 + 3 + 64 / G + 2 * (32 + 4) / G
-    # k_sh_apply: the commit flag and roles byte of every event; owned: per balance side slot 4 +
-    # amount 16 + balance read+write 2 x 16 (no-return 64-bit add), the id owner's record read + append
-    # 2 x 128 and id-table entry 32 unless the window extends the sorted prefix
-    return 2 + (2 * (4 + 16 + 32) + 256 + (0 if prefix else 32)) / G
+# Algorithmic bytes per HOME event of the routed kernels (csrc/route.h) on one of G shards (DESIGN.md
+# §5, §7): with uniform hashing each shard receives about as many messages as it has home events.
+ROUTE_PHASES = {"prep": "route", "resolve": "own", "classify": "decide", "final": "apply"}
+ROUTE_KERNELS = {"prep": ["k_rt_route1<true>", "k_rt_scan", "k_rt_route2<true>"], "resolve": ["k_rt_own<true>"],
+                 "classify": ["k_rt_decide<true>"], "final": ["k_rt_apply<true>"]}
+
+
+def route_kernel_bytes(phase, prefix):
+    """Algorithmic bytes per home event of the routed kernels."""
+    if phase == "prep":
+        # the event read (128, twice: count and scatter passes), the stamped record written to its id
+        # owner's block (128) and two 32 B side messages
+        return 2 * 128 + 128 + 2 * 32
+    if phase == "resolve":
+        # id owner: the record read (128) and a 1 B reply (fresh rising ids probe nothing); account
+        # owners: per side the 32 B message, one 32 B table entry, a 4 B slot and an 8 B reply
+        return 128 + 1 + 2 * (32 + 32 + 4 + 8)
+    if phase == "classify":
+        # per home event: code, owners, positions, ledger (28 B of scratch), three replies (1 + 2 x 8),
+        # three commit bytes, the code written back
+        return 28 + 17 + 3 + 4
+    # apply: per side its commit byte, slot 4, message 32, balance word read + write 2 x 16; per record
+    # its commit byte, read 128 + write 128, id-table entry 32 unless the window extends the sorted prefix
+    return 2 * (1 + 4 + 32 + 32) + 1 + 256 + (0 if prefix else 32) + 8
 
 
 def run_sharded(args, torch, dist, world, rank, device):
-    """cfg5: one global stream, hash-sharded over the ranks (tigerbeetle_amd/sharding.py)."""
+    """cfg5 on N > 1 GPUs: one global stream, hash-sharded over the ranks with partitioned ingestion
+    (tigerbeetle_amd/sharding.py, csrc/route.h): each rank generates and holds only its home batches of
+    every window (1/N of the stream) and the three per-window all-to-alls carry the rest over RCCL."""
     from tigerbeetle_amd import _lib
-    from tigerbeetle_amd.sharding import ShardedStateMachine, exchange_gloo, exchange_nccl
+    from tigerbeetle_amd.sharding import ShardedStateMachine, alltoall_gloo, alltoall_nccl, route_bounds
     from tigerbeetle_amd.state_machine import to_host
     from tigerbeetle_amd.types import Operation
 
     L = _lib.lib()
     G, me = world, rank
     n_acc = args.accounts * G
-    total_batches = (args.transfers * G + BATCH - 1) // BATCH
-    # N > 1: 128-batch windows (each rank is home for 128 / N of them; rehearsal at G = 8 on one GPU:
-    # 5.1G vs 3.3G transfers/s before the collectives, profiles/r1/rehearse_*.json)
-    win = max(1, min(args.window if (args.window_set or G == 1) else WINDOW_BATCHES_MAX, WINDOW_BATCHES_MAX))
+    n_xfer = args.transfers * G
+    total_batches = (n_xfer + BATCH - 1) // BATCH
+    win = max(1, min(args.window, WINDOW_BATCHES_MAX))
     # The whole configured stream is committed (the state always reaches its full size); --warmup
     # batches are untimed and every later batch is timed (>= --steps of them).
     warm = min(((args.warmup + win - 1) // win) * win, max(0, total_batches - win))
     n_batches = total_batches
-    n_xfer = args.transfers * G
-    exchange = None if G == 1 else (exchange_gloo if args.backend == "gloo" else exchange_nccl)
-    acc_cap = n_acc if G == 1 else int(n_acc / G * 1.02) + 65536
-    x_cap = n_xfer if G == 1 else int(n_xfer / G * 1.02) + win * BATCH
-    sm = ShardedStateMachine(G, me, exchange, device=device, batch_max=BATCH, accounts_max=acc_cap,
+    acc_cap = int(n_acc / G * 1.02) + 65536
+    x_cap = int(n_xfer / G * 1.02) + win * BATCH
+    sm = ShardedStateMachine(G, me, None, device=device, batch_max=BATCH, accounts_max=acc_cap,
                              transfers_max=x_cap, window_events_max=win * BATCH)
+    sm.alltoall = alltoall_gloo if args.backend == "gloo" else alltoall_nccl
     stream = sm.sm.stream
 
-    # The whole job's stream, identical and resident on every GPU before timing.
-    d_acc = torch.empty(n_acc * 128, dtype=torch.uint8, device="cuda")
-    d_xfer = torch.empty(n_xfer * 128, dtype=torch.uint8, device="cuda")
+    def home_slices(n_total):
+        """This rank's home batches of every window: (window's first batch, batches, home bounds, event
+        offset of the rank's slice in its home buffer, events)."""
+        nb = (n_total + BATCH - 1) // BATCH
+        out, off = [], 0
+        for b0 in range(0, nb, win):
+            b1 = min(b0 + win, nb)
+            bounds = route_bounds(b1 - b0, G)
+            e0 = min((b0 + bounds[me]) * BATCH, n_total)
+            e1 = min((b0 + bounds[me + 1]) * BATCH, n_total)
+            out.append((b0, b1, bounds, off, e0, e1 - e0))
+            off += e1 - e0
+        return out, off
+
+    # This rank's home slices of the job's stream, resident in HBM before timing (1/N of it).
+    acc_sl, n_acc_home = home_slices(n_acc)
+    x_sl, n_x_home = home_slices(n_xfer)
+    d_acc = torch.empty(max(n_acc_home, 1) * 128, dtype=torch.uint8, device="cuda")
+    d_xfer = torch.empty(max(n_x_home, 1) * 128, dtype=torch.uint8, device="cuda")
     d_res = torch.empty(win * BATCH * 8, dtype=torch.uint8, device="cuda")
-    n_windows_max = (max(n_batches, (n_acc + BATCH - 1) // BATCH) + win - 1) // win + 1
+    n_windows_max = max(len(acc_sl), len(x_sl)) + 1
     d_base = torch.zeros(n_windows_max * (WINDOW_BATCHES_MAX + 1), dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
-    _lib.check(L.tbg_gen_accounts(d_acc.data_ptr(), 0, n_acc, args.seed, 2, 1, 0, stream), "gen accounts")
-    _lib.check(L.tbg_gen_transfers_uniform(d_xfer.data_ptr(), 0, n_xfer, args.seed, n_acc, 0, stream), "gen")
-    _lib.check(L.tbg_gen_permute_ids(d_acc.data_ptr(), n_acc, 0, args.id_order_code, args.perm_seed, stream), "ids")
-    _lib.check(L.tbg_gen_permute_ids(d_xfer.data_ptr(), n_xfer, 1, args.id_order_code, args.perm_seed, stream), "ids")
+    for (_, _, _, off, e0, n) in acc_sl:
+        if n:
+            _lib.check(L.tbg_gen_accounts(d_acc.data_ptr() + off * 128, e0, n, args.seed, 2, 1, 0, stream), "gen")
+            _lib.check(L.tbg_gen_permute_ids(d_acc.data_ptr() + off * 128, n, 0, args.id_order_code, args.perm_seed,
+                                             stream), "ids")
+    for (_, _, _, off, e0, n) in x_sl:
+        if n:
+            _lib.check(L.tbg_gen_transfers_uniform(d_xfer.data_ptr() + off * 128, e0, n, args.seed, n_acc, 0,
+                                                   stream), "gen")
+            _lib.check(L.tbg_gen_permute_ids(d_xfer.data_ptr() + off * 128, n, 1, args.id_order_code, args.perm_seed,
+                                             stream), "ids")
     sm.stream.synchronize()
 
     prepare_ts = 0
 
-    def commit_range(op, d_events, first_batch, last_batch, n_total, widx):
+    def commit_slice(op, d_home, sl, n_total, widx):
         nonlocal prepare_ts
+        b0, b1, bounds, off, _, _ = sl
         ns, ts = [], []
-        for b in range(first_batch, last_batch):
+        for b in range(b0, b1):
             n = min(BATCH, n_total - b * BATCH)
             prepare_ts += 1 + n
             ns.append(n)
             ts.append(prepare_ts)
-        _, count = sm.commit_window(op, d_events.data_ptr() + first_batch * BATCH * 128, ns, ts, d_res.data_ptr(),
-                                    d_base.data_ptr() + widx * (WINDOW_BATCHES_MAX + 1) * 4)
+        _, count = sm.commit_window_routed(op, d_home.data_ptr() + off * 128, ns, ts, d_res.data_ptr(),
+                                           d_base.data_ptr() + widx * (WINDOW_BATCHES_MAX + 1) * 4, bounds)
         return widx, count  # this rank's home batches: d_base[widx, count] = their failures
 
     def failures(wins):
         bases = to_host(d_base).reshape(-1, WINDOW_BATCHES_MAX + 1)
         return int(sum(bases[wi, nb] for wi, nb in wins))
 
-    def barrier():
-        if dist:
-            dist.barrier()
-
-    nb_acc = (n_acc + BATCH - 1) // BATCH
-    wins = [commit_range(Operation.create_accounts, d_acc, b0, min(b0 + win, nb_acc), n_acc, i)
-            for i, b0 in enumerate(range(0, nb_acc, win))]
+    wins = [commit_slice(Operation.create_accounts, d_acc, sl, n_acc, i) for i, sl in enumerate(acc_sl)]
     sm.sync()
     acc_fail = failures(wins)
     d_base.zero_()
 
-    widx = 0
-    warm_windows = []
     NPH = len(PHASES)
+    n_warm_w = warm // win
     L.tbg_timing_collect(sm.h, (ctypes.c_double * NPH)(), (ctypes.c_uint64 * NPH)(), NPH)  # reset
     L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else -1)  # warmup: every phase
-    for b0 in range(0, warm, win):
-        warm_windows.append(commit_range(Operation.create_transfers, d_xfer, b0, min(b0 + win, warm), n_xfer, widx))
-        widx += 1
+    warm_windows = [commit_slice(Operation.create_transfers, d_xfer, x_sl[w], n_xfer, w) for w in range(n_warm_w)]
     sm.sync()
     per_phase, _ = warm_phases(sm, NPH)
-    dom = max(("prep", "final"), key=lambda k: per_phase[k] or 0.0)  # the owned-work and apply kernels
+    dom = max(ROUTE_PHASES, key=lambda k: per_phase[k] or 0.0)
     # timed region: only the roofline kernel's phase records events (two per window)
     L.tbg_timing_enable(sm.h, 0 if args.no_phase_timing else (1 << PHASES.index(dom)))
-    barrier()
+    if dist:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    timed_windows = []
-    for b0 in range(warm, n_batches, win):
-        timed_windows.append(commit_range(Operation.create_transfers, d_xfer, b0, min(b0 + win, n_batches), n_xfer,
-                                          widx))
-        widx += 1
+    timed_windows = [commit_slice(Operation.create_transfers, d_xfer, x_sl[w], n_xfer, w)
+                     for w in range(n_warm_w, len(x_sl))]
     sm.sync()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    barrier()
+    if dist:
+        dist.barrier()
     L.tbg_timing_enable(sm.h, 0)
     ms = (ctypes.c_double * NPH)()
     launches = (ctypes.c_uint64 * NPH)()
     L.tbg_timing_collect(sm.h, ms, launches, NPH)
 
     timed_batches = n_batches - warm
-    timed_events = n_xfer - warm * BATCH  # global: every shard commits the same stream once
+    timed_events = n_xfer - warm * BATCH  # global: the ranks' home slices partition the stream
+    timed_home = sum(x_sl[w][5] for w in range(n_warm_w, len(x_sl)))
     timed_fails = failures(timed_windows)
     fails = failures(warm_windows) + timed_fails
     elapsed = wall
+    dev = "cpu" if args.backend == "gloo" else "cuda"
     if dist:
         # each rank replied for its home batches: failures are summed, the time is the max
-        dev = "cpu" if args.backend == "gloo" else "cuda"
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -552,20 +578,20 @@ def run_sharded(args, torch, dist, world, rank, device):
         di = PHASES.index(dom)
         if launches[di]:
             us = ms[di] / launches[di] * 1000.0
-            ev_per_launch = timed_events / launches[di]
+            ev_per_launch = timed_home / launches[di]
             prefix = st["sorted_transfers"] == st["transfers"]
-            bytes_launch = int(shard_kernel_bytes(dom, G, prefix) * ev_per_launch)
+            bytes_launch = int(route_kernel_bytes(dom, prefix) * ev_per_launch)
             achieved = bytes_launch / (us * 1e-6) / 1e9
-            kname = {"prep": "k_sh_scan<true>", "final": "k_sh_apply<true>"}[dom]
-            tr = pmc_traffic("cfg5", kname, ev_per_launch) if G == 1 else None
-            roof = {"bound": "hbm", "kernel": kname, "events_per_launch": int(ev_per_launch),
-                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
-                    "traffic_fetch_x2": tr[1] if tr else None, "traffic_source": tr[2] if tr else None,
-                    "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
-                    "phase_avg_us_warmup": {k: (round(v, 2) if v else None) for k, v in per_phase.items()},
-                    "exchange_bytes_per_window_per_gpu": int(L.tbg_shard_exchange_bytes(
-                        int(Operation.create_transfers), win * BATCH, G))}
+            kname = ROUTE_KERNELS[dom][0]
+            roof = {"bound": "hbm", "kernel": kname, "phase": ROUTE_PHASES[dom], "phase_kernels": ROUTE_KERNELS[dom],
+                    "events_per_launch": int(ev_per_launch), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "traffic_source": None, "avg_launch_us": round(us, 2), "alg_bytes_per_launch": bytes_launch,
+                    "alg_bytes_basis": "per home event (bench.py route_kernel_bytes)",
+                    "phase_avg_us_warmup": {ROUTE_PHASES[k]: (round(per_phase[k], 2) if per_phase[k] else None)
+                                            for k in ROUTE_PHASES},
+                    # per window and GPU, to the other GPUs: records + sides (A), replies (B), commit bytes (C)
+                    "alltoall_bytes_per_event": round((G - 1) / G * (128 + 2 * 32 + 1 + 2 * 8 + 3), 1)}
         line = {
             "metric": "committed transfers/sec (create_transfers)",
             "value": round(timed_events / elapsed, 1),
@@ -579,26 +605,20 @@ def run_sharded(args, torch, dist, world, rank, device):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u128",
-            "data": "synthetic (device-generated, seed %d, same stream on every GPU)" % args.seed,
-            "config": {"workload": "cfg5: %d accounts hash-sharded over %d GPU(s), %d uniform create_transfers "
+            "data": "synthetic (device-generated, seed %d; each GPU generates and holds its home batches)" % args.seed,
+            "config": {"workload": "cfg5: %d accounts hash-sharded over %d GPUs, %d uniform create_transfers "
                                    "(%.1f %% cross-shard), %d/batch" % (n_acc, G, n_xfer, 100.0 * (G - 1) / G, BATCH),
                        "batch": BATCH, "window_batches": win, "accounts_per_gpu": args.accounts,
                        "id_order": args.id_order, "pending_every": args.pending_every,
                        "transfers_per_gpu": args.transfers,
-                       "parallelism": "hash-sharded accounts+ids, home batch ranges, one RCCL all-reduce "
-                                      "per window (owner facts)" if G > 1 else "single shard"},
+                       "parallelism": "hash-sharded accounts+ids, partitioned ingestion (home batch ranges), "
+                                      "three RCCL all-to-alls per window (route / replies / commit)"},
             "results": {"failed_events_timed": int(timed_fails),
                         "ok_events_per_s": round((timed_events - timed_fails) / elapsed, 1),
                         "shard0_accounts": st["accounts"], "shard0_transfers": st["transfers"],
-                        "backend": args.backend if G > 1 else None, "wall_ms_timed": round(wall * 1000, 3)},
+                        "backend": args.backend, "wall_ms_timed": round(wall * 1000, 3)},
             "roofline": roof,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            import copy
-
-            a2 = copy.copy(args)
-            a2.accounts, a2.transfers = n_acc, n_xfer
-            line["cpu_baseline"] = cpu_baseline(a2, args.seed)
         print(json.dumps(line), flush=True)
     sm.close()
     if dist:
@@ -645,8 +665,9 @@ def main():
     else:
         torch.cuda.set_device(0)
     device = torch.cuda.current_device()
-    if args.config == "cfg5":
+    if args.config == "cfg5" and world > 1:
         return run_sharded(args, torch, dist, world, rank, device)
+    # (cfg5 on one GPU: one shard is the unsharded engine, its fused pass)
 
     from tigerbeetle_amd import StateMachine, _lib, workload
     from tigerbeetle_amd.state_machine import to_host
@@ -835,6 +856,8 @@ def main():
             % (args.pending_every, PENDING_TIMEOUT),
             "cfg3": "cfg3: %d accounts (Zipf 1.2, debits<=credits limits, pre-funded), %d transfers, %d/batch",
             "cfg4": "cfg4: %d accounts, %d two-phase/linked transfers, +1 s per batch, %d/batch",
+            "cfg5": "cfg5 on one GPU (one shard = the unsharded engine): %d accounts, %d uniform create_transfers, "
+                    "%d/batch",
         }[cfg] % (n_acc, n_xfer, BATCH)
         line = {
             "metric": "committed transfers/sec (create_transfers)",

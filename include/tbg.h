@@ -194,6 +194,41 @@ int tbg_shard_prepare_window(tbg_engine *engine, uint32_t operation, const void 
 int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, uint32_t home_first, uint32_t home_count,
                             void *d_results, uint32_t *d_batch_base);
 
+/* Routed sharded commit: partitioned ingestion (tigerbeetle_amd/csrc/route.h). Shard r receives only
+ * the events of its HOME batches [home_bounds[r], home_bounds[r+1]) of the window (home_bounds has
+ * shard_count + 1 entries, home_bounds[0] = 0, home_bounds[G] = n_batches, the same array on every
+ * shard; rank order = batch order), plus the whole window's batch sizes and timestamps. Per window:
+ *   tbg_route_prepare   stamps and validates the home events (state_machine.zig:1253, 1424-1439,
+ *                       1465-1489) and writes one message block per destination shard: the stamped
+ *                       record to the id owner, a 32 B {account id, amount, side} to each account owner;
+ *   exchange A          all-to-all of those blocks (ncclSend/ncclRecv grouped; torch all_to_all_single);
+ *   tbg_route_own       the owners check what they own: id claims (in-window duplicates) and `exists`
+ *                       (:1506-1507, 1450-1460), the accounts (found, ledger, limit / history flags);
+ *   exchange B          all-to-all of the replies back to the homes;
+ *   tbg_route_decide    each home decides its events (:1496-1507, chains :1240-1300): commit bytes;
+ *   exchange C          all-to-all of the commit bytes to the owners;
+ *   tbg_route_apply     home replies (d_results / d_batch_base as tbg_commit_window, for the home batches
+ *                       only) and the owners' effects: balance adds, records appended in timestamp order.
+ * tbg_route_buffers(phase 0 / 1 / 2 = A / B / C) gives the exchange's device buffers: send_bytes[s] bytes
+ * at d_send for shard s, blocks concatenated in shard order, likewise recv_bytes[s] at d_recv from shard s
+ * (the splits of an uneven all-to-all). Each step is asynchronous on the engine stream; the exchanges
+ * must be ordered on it. Class and rejection as tbg_shard_prepare_window's (TBG_E_UNSUPPORTED at
+ * tbg_sync, nothing applied on any shard): the caller then gathers the whole window and commits it
+ * through the general path. Sharded engines of at most 16 shards. */
+int tbg_route_prepare(tbg_engine *engine, uint32_t operation, const void *d_home_events, uint32_t n_batches,
+                      const uint32_t *batch_events, const uint64_t *batch_timestamps, const uint32_t *home_bounds);
+int tbg_route_buffers(tbg_engine *engine, uint32_t phase, void **d_send, uint64_t *send_bytes, void **d_recv,
+                      uint64_t *recv_bytes);
+/* The six exchange buffers (A send, A recv, B send, B recv, C send, C recv) are allocated by the engine
+ * at its first routed window, or are the caller's: tbg_route_buffer_bytes gives their sizes for any
+ * window of at most window_events_max events, tbg_route_attach binds them (16 B-aligned device memory,
+ * e.g. tensors a collective library registers), before the first routed window. */
+int tbg_route_buffer_bytes(tbg_engine *engine, uint64_t *bytes);
+int tbg_route_attach(tbg_engine *engine, void *const *buffers);
+int tbg_route_own(tbg_engine *engine);
+int tbg_route_decide(tbg_engine *engine);
+int tbg_route_apply(tbg_engine *engine, void *d_results, uint32_t *d_batch_base);
+
 /* StateMachine.open (state_machine.zig:527-541), after a restart or a state sync: an empty engine
  * takes the LSM forest's objects: every Account and every Transfer in timestamp order (the grooves'
  * object trees are keyed by timestamp) and, per transfer, its TransferPending status (0 none,

@@ -1,6 +1,7 @@
 """CPU tests of the hash-sharded path (no GPU): the ownership hash matches the library's, and the
-sharded decomposition (owner facts -> all-reduce -> home-batch decide -> all-reduce of commit flags
--> owned effects) reproduces the CPU restatement, with real gloo collectives at world size 2 and 3."""
+routed decomposition of csrc/route.h (home route -> all-to-all -> owners' replies -> all-to-all ->
+home decide -> all-to-all of commit bytes -> owned effects, tests/shard_model.py) reproduces the CPU
+restatement, with real gloo all-to-alls at world size 2 and 3."""
 import os
 import socket
 
@@ -74,40 +75,55 @@ def _stream(seed, n_acc, n_batches):
     return out
 
 
-def _rank(rank, world, port, seed, n_acc, n_batches, out_dir):
+def _alltoall(blocks, world):
+    """Uneven all-to-all of byte blocks (blocks[d] goes to rank d): gloo all_to_all_single."""
     import torch
     import torch.distributed as dist
 
+    send_sizes = [len(b) for b in blocks]
+    recv_sizes = torch.zeros(world, dtype=torch.int64)
+    dist.all_to_all_single(recv_sizes, torch.tensor(send_sizes, dtype=torch.int64))
+    recv_sizes = recv_sizes.tolist()
+    send = torch.from_numpy(np.frombuffer(b"".join(blocks), np.uint8).copy())
+    recv = torch.empty(sum(recv_sizes), dtype=torch.uint8)
+    dist.all_to_all_single(recv, send, recv_sizes, send_sizes)
+    r = recv.numpy().tobytes()
+    out, o = [], 0
+    for n in recv_sizes:
+        out.append(r[o: o + n])
+        o += n
+    return out
+
+
+def _rank(rank, world, port, seed, n_acc, n_batches, out_dir):
+    import torch.distributed as dist
+
     from shard_model import ShardModel
+    from tigerbeetle_amd.sharding import route_bounds
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from shard_model import ca_static, ct_static
-    from tigerbeetle_amd.sharding import home_range
-
     m = ShardModel(world, rank)
     T, mine = 0, {}
     for wi, (op, batches) in enumerate(_windows(seed, n_acc, n_batches)):
-        events = np.concatenate(batches)
-        offs, ts = np.cumsum([0] + [len(b) for b in batches]), []
+        ts = []
         for ev in batches:
             T += 1 + len(ev)
-            ts += [T - len(ev) + j + 1 for j in range(len(ev))]
-        words, _ = m.prep(op, events)
-        w = torch.from_numpy(words)
-        dist.all_reduce(w)  # exchange 1: owner facts summed across shards
-        first, count = home_range(len(batches), world, rank)
-        commit = torch.zeros(len(events), dtype=torch.int32)
-        for b in range(first, first + count):
-            ev = batches[b]
-            wb = np.concatenate([w.numpy()[:1], w.numpy()[1 + offs[b]: 1 + offs[b + 1]]])
-            static = [ca_static(e) if op == "a" else ct_static(e) for e in ev]
-            codes = m.decide(op, ev, wb, static)
-            commit[offs[b]: offs[b + 1]] = torch.tensor([c == 0 for c in codes], dtype=torch.int32)
-            mine[(wi, b)] = np.array([(i, c) for i, c in enumerate(codes) if c != 0], np.uint32).reshape(-1, 2)
-        dist.all_reduce(commit)  # exchange 2: commit flags of every home's events
-        m.apply(op, events, commit.numpy(), ts)
+            ts.append(T)
+        bounds = route_bounds(len(batches), world)
+        if wi % 3 == 2:  # uneven homes: one shard home for the whole window
+            bounds = [0] * (world - 1 - wi % world) + [len(batches)] * (2 + wi % world)
+            bounds = bounds[: world + 1]
+            bounds[0] = 0
+            bounds[-1] = len(batches)
+        recv_a = _alltoall(m.route(op, batches, ts, bounds), world)
+        recv_b = _alltoall(m.own(recv_a), world)
+        replies, c = m.decide(recv_b)
+        recv_c = _alltoall(c, world)
+        assert m.apply(recv_c) == 0
+        for k, b in enumerate(range(bounds[rank], bounds[rank + 1])):
+            mine[(wi, b)] = np.frombuffer(replies[k], np.uint32).reshape(-1, 2)
     np.save(os.path.join(out_dir, f"acc{rank}.npy"), np.array(list(m.accounts.values())))
     np.save(os.path.join(out_dir, f"xfer{rank}.npy"), np.array(list(m.transfers.values())))
     keys = sorted(mine)

@@ -25,7 +25,8 @@ EXPORTS = [
     "tbg_gw_collect", "tbg_gw_write", "tbg_gw_commit", "tbg_gw_result",
     "tbg_shard_apply", "tbg_open_device", "tbg_device_state", "tbg_device_history", "tbg_shard_lookup_bytes",
     "tbg_shard_lookup", "tbg_shard_lookup_reply", "tbg_shard_query_bytes", "tbg_shard_query", "tbg_shard_query_merge",
-    "tbg_debug_table_used",
+    "tbg_debug_table_used", "tbg_route_prepare", "tbg_route_buffers", "tbg_route_buffer_bytes", "tbg_route_attach", "tbg_route_own", "tbg_route_decide",
+    "tbg_route_apply",
 ]
 
 
@@ -167,6 +168,13 @@ def lib():
         "tbg_shard_query_merge": ([vp, u32, vp, vp, vp, u64, P(u64)], i32),
         "tbg_open_device": ([vp, vp, u64, vp, vp, u64, u64], i32),
         "tbg_device_state": ([vp, P(vp), P(u64), P(vp), P(vp), P(u64), P(u64)], i32),
+        "tbg_route_prepare": ([vp, u32, vp, u32, vp, vp, vp], i32),
+        "tbg_route_buffers": ([vp, u32, P(vp), vp, P(vp), vp], i32),
+        "tbg_route_buffer_bytes": ([vp, vp], i32),
+        "tbg_route_attach": ([vp, vp], i32),
+        "tbg_route_own": ([vp], i32),
+        "tbg_route_decide": ([vp], i32),
+        "tbg_route_apply": ([vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

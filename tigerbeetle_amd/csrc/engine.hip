@@ -1448,6 +1448,7 @@ __global__ void __launch_bounds__(SEG) k_final(Dev d, Scratch s, const uint8_t* 
 
 #include "fused.h"
 #include "shard.h"
+#include "route.h"
 
 // ------------------------------------------------------------------------------------------------
 // Pulse: ExpirePendingTransfers scan + execute_expire_pending_transfers (state_machine.zig:
@@ -1761,3 +1762,4 @@ __global__ void k_setup(Dev d, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dp
 #include "shard_gx.inc"
 #include "shard_gw.inc"
 #include "shard_read.inc"
+#include "route.inc"

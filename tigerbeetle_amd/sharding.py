@@ -76,6 +76,33 @@ def exchange_gloo(t):
     torch.cuda.current_stream().synchronize()
 
 
+def alltoall_nccl(send, send_sizes, recv, recv_sizes):
+    """Uneven all-to-all of byte blocks across the process group on the current (engine) stream:
+    grouped ncclSend / ncclRecv under RCCL (torch "nccl" on ROCm)."""
+    import torch.distributed as dist
+
+    dist.all_to_all_single(recv, send, list(recv_sizes), list(send_sizes))
+
+
+def alltoall_gloo(send, send_sizes, recv, recv_sizes):
+    """The same through host memory (gloo): for ranks that share one GPU in tests."""
+    import torch
+    import torch.distributed as dist
+
+    s = torch.empty(send.shape, dtype=send.dtype, pin_memory=True)
+    s.copy_(send, non_blocking=True)
+    torch.cuda.current_stream().synchronize()
+    r = torch.empty(recv.shape, dtype=recv.dtype)
+    dist.all_to_all_single(r, s, list(recv_sizes), list(send_sizes))
+    recv.copy_(r, non_blocking=True)
+    torch.cuda.current_stream().synchronize()
+
+
+def route_bounds(n_batches, shard_count):
+    """Home batch bounds of a routed window: shard r is home for [bounds[r], bounds[r + 1])."""
+    return [n_batches * r // shard_count for r in range(shard_count + 1)]
+
+
 class _timed:
     """(rehearsal) wall time of a general-window step on this shard, synced, when gw_times is set:
     slots 0-1 phase 1 (collect, write), 2-3 phase 2, 4 commit (scratch engine + apply)."""
@@ -140,6 +167,8 @@ class ShardedStateMachine:
         self.gw_times = None  # (rehearsal: tools/rehearse_shards.py) per-step wall times of general windows
         self.gw_fallbacks = {"due_overflow": 0, "rejected": 0}  # general windows sent batch by batch
         self.gw_acc_base = None  # accounts the general windows' scratch engine holds (None: starts over)
+        self.rt = None           # routed windows: the six exchange buffers (attached at the first one)
+        self.alltoall = None     # routed windows: this process's all-to-all (alltoall_nccl / alltoall_gloo)
         torch.cuda.synchronize(device)
 
     @property
@@ -155,6 +184,84 @@ class ShardedStateMachine:
 
     def home_range(self, n_batches):
         return home_range(n_batches, self.shard_count, self.shard_index)
+
+    # --------------------------------------------------------------------------------------------
+    # Routed windows (csrc/route.h): partitioned ingestion. This shard holds only its home batches'
+    # events; three all-to-alls carry the messages to the owners, their replies to the homes and the
+    # commit bytes back to the owners.
+    # --------------------------------------------------------------------------------------------
+    def _route_init(self):
+        import torch
+
+        if getattr(self, "rt", None) is not None:
+            return
+        L = _lib.lib()
+        b = (ctypes.c_uint64 * 6)()
+        _lib.check(L.tbg_route_buffer_bytes(self.sm.h, b), "route_buffer_bytes")
+        dev = torch.device("cuda", self.device)
+        self.rt = [torch.empty(max(int(x), 16), dtype=torch.uint8, device=dev) for x in b]
+        torch.cuda.synchronize(self.device)
+        ptrs = (ctypes.c_void_p * 6)(*[t.data_ptr() for t in self.rt])
+        _lib.check(L.tbg_route_attach(self.sm.h, ptrs), "route_attach")
+
+    def route_prepare(self, operation, d_home_events, batch_events, batch_timestamps, bounds=None):
+        """Step 1 of a routed window: this shard's home events (batches [bounds[me], bounds[me + 1]),
+        contiguous at d_home_events) routed into message blocks. Returns (home_first, home_count)."""
+        self._route_init()
+        self.invalidate_scratch()
+        nb = len(batch_events)
+        bounds = bounds or route_bounds(nb, self.shard_count)
+        ev = (ctypes.c_uint32 * nb)(*batch_events)
+        ts = (ctypes.c_uint64 * nb)(*batch_timestamps)
+        hb = (ctypes.c_uint32 * (self.shard_count + 1))(*bounds)
+        _lib.check(_lib.lib().tbg_route_prepare(self.sm.h, int(operation), d_home_events, nb, ev, ts, hb),
+                   "route_prepare")
+        r = self.shard_index
+        return bounds[r], bounds[r + 1] - bounds[r]
+
+    def route_views(self, phase):
+        """The exchange of phase 0 / 1 / 2 (A / B / C): (send, send_sizes, recv, recv_sizes), uint8
+        views of the attached buffers: the splits of an uneven all-to-all."""
+        G = self.shard_count
+        sp, rp = ctypes.c_void_p(), ctypes.c_void_p()
+        ss, rs = (ctypes.c_uint64 * G)(), (ctypes.c_uint64 * G)()
+        _lib.check(_lib.lib().tbg_route_buffers(self.sm.h, phase, ctypes.byref(sp), ss, ctypes.byref(rp), rs),
+                   "route_buffers")
+        send_t = self.rt[2 * phase]
+        recv_t = self.rt[2 * phase + 1]
+        assert sp.value == send_t.data_ptr() and rp.value == recv_t.data_ptr()
+        ss, rs = [int(x) for x in ss], [int(x) for x in rs]
+        return send_t[: sum(ss)], ss, recv_t[: sum(rs)], rs
+
+    def route_step(self, step):
+        """Steps 2-4 between the exchanges: "own", "decide"."""
+        fn = {"own": _lib.lib().tbg_route_own, "decide": _lib.lib().tbg_route_decide}[step]
+        _lib.check(fn(self.sm.h), "route_" + step)
+
+    def route_apply(self, d_results, d_batch_base):
+        _lib.check(_lib.lib().tbg_route_apply(self.sm.h, d_results, d_batch_base), "route_apply")
+
+    def commit_window_routed(self, operation, d_home_events, batch_events, batch_timestamps, d_results,
+                             d_batch_base, bounds=None):
+        """A routed window with this process's all-to-all (`alltoall(send, send_sizes, recv, recv_sizes)`),
+        asynchronous on the engine stream. Replies of the home batches land in d_results / d_batch_base;
+        returns (home_first, home_count). The harness pulse before the first batch must have run (no
+        pulse may fall due inside the window: the window is rejected otherwise)."""
+        import torch
+
+        first, count = self.route_prepare(operation, d_home_events, batch_events, batch_timestamps, bounds)
+        for phase, step in ((0, "own"), (1, "decide"), (2, None)):
+            if self.alltoall is not None:
+                with torch.cuda.stream(self.stream):
+                    self.alltoall(*self.route_views(phase))
+            else:  # (one shard: its only block is its own)
+                send, ss, recv, rs = self.route_views(phase)
+                with torch.cuda.stream(self.stream):
+                    recv.copy_(send)
+            if step:
+                self.route_step(step)
+        self.route_apply(d_results, d_batch_base)
+        return first, count
 
     def prepare_window(self, operation, d_events, batch_events, batch_timestamps):
         """Step 1; returns the facts tensor to be summed across the shards."""
@@ -635,3 +742,42 @@ def commit_general_batch(shards, summed, operation, d_events, n, timestamp, auto
     replies = [s.decide_apply(operation, d_events, n, timestamp, auto_pulse) for s in shards]
     assert all(r == replies[0] for r in replies), "shards decided the batch differently"
     return replies[0]
+
+
+def route_exchange_inprocess(shards, phase):
+    """The all-to-all of a routed window's phase among shards of this process (one GPU): block
+    [src -> dst] of src's send buffer into dst's receive buffer at src's offset."""
+    import torch
+
+    views = [s.route_views(phase) for s in shards]
+    for s in shards:  # (engine streams are non-blocking: wait for each explicitly)
+        s.stream.synchronize()
+    G = len(shards)
+    for src in range(G):
+        send, ss = views[src][0], views[src][1]
+        soff = 0
+        for dst in range(G):
+            recv, rs = views[dst][2], views[dst][3]
+            assert rs[src] == ss[dst], (phase, src, dst, rs[src], ss[dst])
+            roff = sum(rs[:src])
+            recv[roff: roff + ss[dst]].copy_(send[soff: soff + ss[dst]])
+            soff += ss[dst]
+    torch.cuda.synchronize()
+
+
+def commit_routed_inprocess(shards, operation, home_events, batch_events, batch_timestamps, results, bases,
+                            bounds=None):
+    """A routed window over the shards of this process: home_events[r] = the device pointer of shard r's
+    home events; results[r] / bases[r] its reply buffers. Returns each shard's (home_first, home_count)."""
+    G = len(shards)
+    bounds = bounds or route_bounds(len(batch_events), G)
+    homes = [s.route_prepare(operation, home_events[r], batch_events, batch_timestamps, bounds)
+             for r, s in enumerate(shards)]
+    for phase, step in ((0, "own"), (1, "decide"), (2, None)):
+        route_exchange_inprocess(shards, phase)
+        if step:
+            for s in shards:
+                s.route_step(step)
+    for r, s in enumerate(shards):
+        s.route_apply(results[r], bases[r])
+    return homes

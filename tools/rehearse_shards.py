@@ -1,9 +1,10 @@
 """Per-shard GPU time of the hash-sharded commit at G shards, rehearsed on ONE GPU.
 
-G ShardedStateMachine engines live on cuda:0 in this process. Each window runs shard by shard
-(prepare -> in-process byte-wise sum of the facts, i.e. what the RCCL all-reduce computes -> commit:
-decide every event, reply for the home batches, apply the owned effects), with HIP events on each
-engine's stream around each step. A shard's GPU time per window is what one GPU of a G-GPU node
+G ShardedStateMachine engines live on cuda:0 in this process. Each window runs shard by shard, with
+HIP events on each engine's stream around each step: --protocol routed (default; csrc/route.h) routes
+each shard's home slice, then own / decide / apply between in-process all-to-alls; --protocol
+replicated (csrc/shard.h) prepares the whole window on every shard, sums the facts in-process (what the
+RCCL all-reduce computes) and commits. A shard's GPU time per window is what one GPU of a G-GPU node
 spends on the window apart from the collective, so
 
     estimated G-GPU rate = global events / sum over windows of max over shards (prepare + commit)
@@ -153,6 +154,9 @@ def main():
     p.add_argument("--window", type=int, default=64, help="batches per (global) window")
     p.add_argument("--warmup", type=int, default=2, help="untimed windows")
     p.add_argument("--seed", type=int, default=47)
+    p.add_argument("--protocol", default="routed", choices=["routed", "replicated"],
+                   help="cfg5: routed = partitioned ingestion (csrc/route.h); replicated = every shard holds "
+                        "the window, one all-reduce of facts (csrc/shard.h)")
     p.add_argument("--stream", default="cfg5", choices=["cfg5", "cfg3", "cfg4"],
                    help="cfg5: the order-free fast path; cfg3 / cfg4: the general class a window at a time")
     a = p.parse_args()
@@ -205,8 +209,46 @@ def main():
             t.copy_(total)
         torch.cuda.synchronize()
 
+    routed = a.protocol == "routed"
+    xbytes = []  # routed: per window, the bytes each shard sends to the others (max over shards)
+
+    def window_routed(op, d_ev, b0, b1, n_total, timed):
+        """Partitioned ingestion (csrc/route.h): shard r reads only its home batches (a contiguous
+        slice of the stream); the three all-to-alls are in-process block copies (not timed)."""
+        nonlocal prepare_ts
+        from tigerbeetle_amd.sharding import route_bounds, route_exchange_inprocess
+
+        ns, ts = [], []
+        for b in range(b0, b1):
+            n = min(BATCH, n_total - b * BATCH)
+            prepare_ts += 1 + n
+            ns.append(n)
+            ts.append(prepare_ts)
+        bounds = route_bounds(len(ns), G)
+        homes = [d_ev.data_ptr() + (b0 + bounds[r]) * BATCH * 128 for r in range(G)]
+        _, ev1 = timed_step(lambda r, s: s.route_prepare(op, homes[r], ns, ts, bounds))
+        sent = 0
+        for phase in range(3):
+            views = [s.route_views(phase) for s in shards]
+            sent += max(sum(v[1]) - v[1][r] for r, v in enumerate(views))
+            route_exchange_inprocess(shards, phase)
+            if phase == 0:
+                _, ev2 = timed_step(lambda r, s: s.route_step("own"))
+            elif phase == 1:
+                _, ev3 = timed_step(lambda r, s: s.route_step("decide"))
+        _, ev4 = timed_step(lambda r, s: s.route_apply(d_res.data_ptr() + r * (d_res.numel() // G // 16 * 16),
+                                                       d_base.data_ptr() + r * 256 * 4))
+        for s in shards:
+            s.sync()
+        if timed:
+            times.append([tuple(e[0].elapsed_time(e[1]) for e in evs) for evs in zip(ev1, ev2, ev3, ev4)])
+            xbytes.append(sent)
+        return sum(ns)
+
     def window(op, d_ev, b0, b1, n_total, timed):
         nonlocal prepare_ts
+        if routed:
+            return window_routed(op, d_ev, b0, b1, n_total, timed)
         ns, ts = [], []
         for b in range(b0, b1):
             n = min(BATCH, n_total - b * BATCH)
@@ -237,9 +279,24 @@ def main():
         n = window(Operation.create_transfers, d_x, b0, min(b0 + win, nb), n_x, k >= a.warmup)
         if k >= a.warmup:
             events += n
-    t = np.array(times)  # windows x shards x (scan, decide + apply), ms
+    t = np.array(times)  # windows x shards x steps, ms
     per_shard = t.sum(axis=2)
     crit = per_shard.max(axis=1).sum() / 1000.0
+    if routed:
+        names = ["route", "own", "decide", "apply"]
+        out = {
+            "protocol": "routed", "shards": G, "window_batches": win, "timed_windows": len(times),
+            "events_timed": events,
+            "shard_ms_per_window": dict({n + "_mean": round(float(t[:, :, k].mean()), 4) for k, n in enumerate(names)},
+                                        max_shard_mean=round(float(per_shard.max(axis=1).mean()), 4)),
+            "estimated_rate_excl_collective": round(events / crit, 1),
+            "alltoall_bytes_per_window_per_gpu_max": int(np.mean(xbytes)),
+            "stats_shard0": shards[0].stats(),
+        }
+        print(json.dumps(out), flush=True)
+        for s in shards:
+            s.close()
+        return
     out = {
         "shards": G, "window_batches": win, "timed_windows": len(times), "events_timed": events,
         "shard_ms_per_window": {"scan_mean": round(float(t[:, :, 0].mean()), 4),
