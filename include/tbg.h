@@ -229,6 +229,46 @@ int tbg_route_own(tbg_engine *engine);
 int tbg_route_decide(tbg_engine *engine);
 int tbg_route_apply(tbg_engine *engine, void *d_results, uint32_t *d_batch_base);
 
+/* A hash-sharded group: G engines (one per GPU, or several on one GPU for tests) behind the
+ * StateMachine interface, driven by one host thread (tigerbeetle_amd/csrc/group.inc). The replacement
+ * for the reference's single StateMachine when accounts are partitioned across the GPUs of a node: a
+ * replica calls tbg_group_pulse_needed / tbg_group_prefetch / tbg_group_commit exactly where it calls
+ * pulse() / prefetch() / commit() (vsr/replica.zig:3764-3772, 4149-4159, 9459-9487), with the same
+ * reply bytes as one engine. create_* batches go through the routed order-free path (tbg_route_*) and,
+ * outside its class, through the general path (gathers, a scratch engine per shard, tbg_shard_apply);
+ * pulses and lookups / queries gather from the owners. The exchanges are the group's own: device copies
+ * (TBG_EXCHANGE_COPY) or one RCCL communicator per GPU (TBG_EXCHANGE_RCCL: ncclCommInitAll over the G
+ * devices, librccl opened at creation; grouped ncclAllReduce / ncclSend / ncclRecv on the engine
+ * streams). accounts_max / transfers_max are per shard. tbg_group_commit_window commits host-resident
+ * batches under the harness protocol (a pulse check before every batch, state_machine.zig:2719-2739),
+ * replies as tbg_commit_window's into host buffers. tbg_group_engine names shard r's engine (dumps,
+ * stats, digests of its part of the state). */
+typedef struct tbg_group tbg_group;
+#define TBG_EXCHANGE_COPY 0u
+#define TBG_EXCHANGE_RCCL 1u
+typedef struct tbg_group_config {
+    uint32_t shard_count;      /* G, 1..16 */
+    uint32_t exchange;         /* TBG_EXCHANGE_* */
+    const int32_t *devices;    /* G HIP device ordinals (RCCL: distinct) */
+    uint32_t batch_max;        /* 0 = 8190 */
+    uint32_t window_events_max;
+    uint64_t accounts_max;     /* per shard */
+    uint64_t transfers_max;    /* per shard */
+    uint32_t flags;            /* TBG_FLAG_* of the shard engines */
+    uint32_t reserved;
+} tbg_group_config;
+int tbg_group_create(const tbg_group_config *config, tbg_group **out);
+int tbg_group_destroy(tbg_group *group);
+int tbg_group_pulse_needed(tbg_group *group, uint64_t prepare_timestamp, int *needed);
+int tbg_group_prefetch(tbg_group *group, uint64_t op, uint32_t operation, const void *input, uint64_t input_len,
+                       uint64_t prefetch_timestamp);
+int tbg_group_commit(tbg_group *group, uint64_t op, uint64_t timestamp, uint32_t operation, const void *input,
+                     uint64_t input_len, void *output, uint64_t output_cap, uint64_t *output_len);
+int tbg_group_commit_window(tbg_group *group, uint32_t operation, const void *h_events, uint32_t n_batches,
+                            const uint32_t *batch_events, const uint64_t *batch_timestamps, void *h_results,
+                            uint32_t *h_batch_base);
+int tbg_group_engine(tbg_group *group, uint32_t shard, tbg_engine **engine);
+
 /* StateMachine.open (state_machine.zig:527-541), after a restart or a state sync: an empty engine
  * takes the LSM forest's objects: every Account and every Transfer in timestamp order (the grooves'
  * object trees are keyed by timestamp) and, per transfer, its TransferPending status (0 none,

@@ -203,3 +203,95 @@ def test_route_rejects_windows_outside_class(kind):
         assert sh.commit_window(Operation.create_transfers, [t[40:50], t[50:]]) == [b"", b""]
     finally:
         sh.close()
+
+
+def _defined(phase, blk, L, src, dst, n_id, n_side):
+    """The bytes of a message block that the protocol defines (padding and unused capacity excluded):
+    `src` is the block's HOME shard (its layout), `dst` the owner."""
+    if phase == 0:
+        s0 = 256 + L.c1[src] * 128
+        return blk[:48] + blk[256: 256 + n_id * 128] + blk[s0: s0 + n_side * 32]
+    if phase == 1:
+        return blk[:4] + blk[64: 64 + n_id] + blk[L.b_side(src): L.b_side(src) + n_side * 8]
+    return (blk[:4] + blk[64: 64 + 4 * L.nch(src)] + blk[L.c_hdr(src): L.c_hdr(src) + n_id] +
+            blk[L.c_side(src): L.c_side(src) + n_side])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [2, 3])
+def test_route_blocks_match_cpu_model(G):
+    """The engine's message blocks of every exchange are byte-equal (in every defined byte) to the CPU
+    model's (tests/shard_model.py), window after window of a mixed stream; stores equal the oracle's."""
+    import struct
+
+    import torch
+
+    from shard_model import ShardModel
+    from test_shard_cpu import BM as MBM
+    from test_shard_cpu import _windows
+    from tigerbeetle_amd.sharding import route_bounds, route_exchange_inprocess
+
+    sh = RoutedShards(G, MBM, 1024, 1 << 14, 3 * MBM)
+    models = [ShardModel(G, r) for r in range(G)]
+    ref = OracleStateMachine(batch_max=MBM)
+    T = 0
+    try:
+        for wi, (op, batches) in enumerate(_windows(5, 150, 30)):
+            ts = []
+            for ev in batches:
+                T += 1 + len(ev)
+                ts.append(T)
+            oracle_batches(ref, Operation.create_accounts if op == "a" else Operation.create_transfers, batches)
+            bounds = route_bounds(len(batches), G) if wi % 2 else [0] + [len(batches)] * G
+            keep, res, bases = [], [], []
+            for r, s in enumerate(sh.shards):
+                part = batches[bounds[r]:bounds[r + 1]]
+                data = np.concatenate([np.frombuffer(e.tobytes(), np.uint8) for e in part]) if part else np.zeros(128, np.uint8)
+                d_ev = torch.from_numpy(data.copy()).cuda()
+                keep.append(d_ev)
+                res.append(torch.zeros(4096, dtype=torch.uint8).cuda())
+                bases.append(torch.zeros(8, dtype=torch.int32).cuda())
+            torch.cuda.synchronize()
+            operation = Operation.create_accounts if op == "a" else Operation.create_transfers
+            sh.pulse_before(ts[0])  # (the harness pulse: afterwards none is due inside the window)
+            for r, s in enumerate(sh.shards):
+                s.route_prepare(operation, keep[r].data_ptr(), [len(b) for b in batches], ts, bounds)
+            sent = [m.route(op, batches, ts, bounds) for m in models]
+            L = models[0].L
+            counts = [[struct.unpack_from("<II", sent[s][d], 0) for d in range(G)] for s in range(G)]
+            for phase in range(3):
+                for s in sh.shards:
+                    s.stream.synchronize()
+                for src in range(G):
+                    send, ss, _, _ = sh.shards[src].route_views(phase)
+                    dev = to_host(send).tobytes()
+                    off = 0
+                    for dst in range(G):
+                        blk = dev[off: off + ss[dst]]
+                        off += ss[dst]
+                        n_id, n_side = counts[src][dst] if phase != 1 else counts[dst][src]
+                        want = _defined(phase, sent[src][dst], L, src if phase != 1 else dst, dst if phase != 1 else src,
+                                        n_id, n_side)
+                        got = _defined(phase, blk, L, src if phase != 1 else dst, dst if phase != 1 else src,
+                                       n_id, n_side)
+                        assert got == want, f"window {wi} phase {phase} block {src}->{dst}"
+                route_exchange_inprocess(sh.shards, phase)
+                recv = [[sent[s][d] for s in range(G)] for d in range(G)]
+                if phase == 0:
+                    for s in sh.shards:
+                        s.route_step("own")
+                    sent = [m.own(recv[r]) for r, m in enumerate(models)]
+                elif phase == 1:
+                    for s in sh.shards:
+                        s.route_step("decide")
+                    sent = [m.decide(recv[r])[1] for r, m in enumerate(models)]
+                else:
+                    for r, s in enumerate(sh.shards):
+                        s.route_apply(res[r].data_ptr(), bases[r].data_ptr())
+                    assert all(m.apply(recv[r]) == 0 for r, m in enumerate(models))
+            for s in sh.shards:
+                s.sync()
+        _compare_sharded(sh, ref)
+    finally:
+        sh.close()
+        ref.close()

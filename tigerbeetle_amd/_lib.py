@@ -26,7 +26,8 @@ EXPORTS = [
     "tbg_shard_apply", "tbg_open_device", "tbg_device_state", "tbg_device_history", "tbg_shard_lookup_bytes",
     "tbg_shard_lookup", "tbg_shard_lookup_reply", "tbg_shard_query_bytes", "tbg_shard_query", "tbg_shard_query_merge",
     "tbg_debug_table_used", "tbg_route_prepare", "tbg_route_buffers", "tbg_route_buffer_bytes", "tbg_route_attach", "tbg_route_own", "tbg_route_decide",
-    "tbg_route_apply",
+    "tbg_route_apply", "tbg_group_create", "tbg_group_destroy", "tbg_group_pulse_needed", "tbg_group_prefetch",
+    "tbg_group_commit", "tbg_group_commit_window", "tbg_group_engine",
 ]
 
 
@@ -52,6 +53,17 @@ FLAG_CHANGE_LOG = 8
 FLAG_NO_XWIN = 16
 FLAG_NO_CHUNKS = 32
 FLAG_NO_FUSED = 64
+
+
+class GroupConfig(ctypes.Structure):
+    _fields_ = [("shard_count", ctypes.c_uint32), ("exchange", ctypes.c_uint32),
+                ("devices", ctypes.POINTER(ctypes.c_int32)), ("batch_max", ctypes.c_uint32),
+                ("window_events_max", ctypes.c_uint32), ("accounts_max", ctypes.c_uint64),
+                ("transfers_max", ctypes.c_uint64), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+EXCHANGE_COPY = 0
+EXCHANGE_RCCL = 1
 
 
 class Stats(ctypes.Structure):
@@ -175,6 +187,13 @@ def lib():
         "tbg_route_own": ([vp], i32),
         "tbg_route_decide": ([vp], i32),
         "tbg_route_apply": ([vp, vp, vp], i32),
+        "tbg_group_create": ([P(GroupConfig), P(vp)], i32),
+        "tbg_group_destroy": ([vp], i32),
+        "tbg_group_pulse_needed": ([vp, u64, P(ctypes.c_int)], i32),
+        "tbg_group_prefetch": ([vp, u64, u32, vp, u64, u64], i32),
+        "tbg_group_commit": ([vp, u64, u64, u32, vp, u64, vp, u64, P(u64)], i32),
+        "tbg_group_commit_window": ([vp, u32, vp, u32, vp, vp, vp, vp], i32),
+        "tbg_group_engine": ([vp, u32, P(vp)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -1763,3 +1763,4 @@ __global__ void k_setup(Dev d, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dp
 #include "shard_gw.inc"
 #include "shard_read.inc"
 #include "route.inc"
+#include "group.inc"

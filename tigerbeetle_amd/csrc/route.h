@@ -484,21 +484,20 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
       const uint8_t* rec = rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)k * 128;
       uint32_t code;
       bool dup = false;
+      // the id only (16 B): the rest of the record is read when a stored one must be compared
+      const tb_uint128_t id = rw_u128(*reinterpret_cast<const uint4*>(rec));
+      if (sh_claim) dup = rt_claim(rb.claim, rb.claim_mask, epoch, rt_id_base(L, sg) + k, id, rb.a_recv, L);
       if (XFER) {
-        const tb_transfer_t t = *reinterpret_cast<const tb_transfer_t*>(rec);
-        if (sh_claim) dup = rt_claim(rb.claim, rb.claim_mask, epoch, rt_id_base(L, sg) + k, t.id, rb.a_recv, L);
         uint32_t xs = NONE32;
-        if (x_may_exist(t.id, g->x_id_max)) {
-          xs = x_find(d.x_tab, d.xr, d.x_mask, t.id);
-          if (xs == NONE32) xs = x_prefix_find(d.xr, g->x_sorted, t.id);
+        if (x_may_exist(id, g->x_id_max)) {
+          xs = x_find(d.x_tab, d.xr, d.x_mask, id);
+          if (xs == NONE32) xs = x_prefix_find(d.xr, g->x_sorted, id);
         }
-        code = xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(t, d.xr[xs]);
+        code = xs == NONE32 ? (uint32_t)TB_CT_OK : ct_exists(*reinterpret_cast<const tb_transfer_t*>(rec), d.xr[xs]);
       } else {
-        const tb_account_t a = *reinterpret_cast<const tb_account_t*>(rec);
-        dup = rt_claim(rb.claim, rb.claim_mask, epoch, rt_id_base(L, sg) + k, a.id, rb.a_recv, L);
         AccEntry ae;
-        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, a.id, &ae);
-        code = slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(a, d.acc[slot]);
+        const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, id, &ae);
+        code = slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(*reinterpret_cast<const tb_account_t*>(rec), d.acc[slot]);
       }
       rb.b_send[rt_off_b(L, sg) + RT_HDR_B + k] = (uint8_t)((1u + code) | (dup ? RI_DUP : 0u));
     }
