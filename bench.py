@@ -457,7 +457,8 @@ def run_sharded(args, torch, dist, world, rank, device):
     n_acc = args.accounts * G
     n_xfer = args.transfers * G
     total_batches = (n_xfer + BATCH - 1) // BATCH
-    win = max(1, min(args.window, WINDOW_BATCHES_MAX))
+    # a routed window holds up to 128 batches per home: G x 128 by default (one home slice = 1M events)
+    win = max(1, min(args.window if args.window_set else WINDOW_BATCHES_MAX * G, WINDOW_BATCHES_MAX * G))
     # The whole configured stream is committed (the state always reaches its full size); --warmup
     # batches are untimed and every later batch is timed (>= --steps of them).
     warm = min(((args.warmup + win - 1) // win) * win, max(0, total_batches - win))

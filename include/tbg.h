@@ -214,7 +214,8 @@ int tbg_shard_commit_window(tbg_engine *engine, const void *d_exchange, uint32_t
  * (the splits of an uneven all-to-all). Each step is asynchronous on the engine stream; the exchanges
  * must be ordered on it. Class and rejection as tbg_shard_prepare_window's (TBG_E_UNSUPPORTED at
  * tbg_sync, nothing applied on any shard): the caller then gathers the whole window and commits it
- * through the general path. Sharded engines of at most 16 shards. */
+ * through the general path. Sharded engines of at most 16 shards. A routed window holds up to G x 128
+ * batches, each home's part at most 128 batches and window_events_max events. */
 int tbg_route_prepare(tbg_engine *engine, uint32_t operation, const void *d_home_events, uint32_t n_batches,
                       const uint32_t *batch_events, const uint64_t *batch_timestamps, const uint32_t *home_bounds);
 int tbg_route_buffers(tbg_engine *engine, uint32_t phase, void **d_send, uint64_t *send_bytes, void **d_recv,
