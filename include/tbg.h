@@ -174,8 +174,12 @@ int tbg_read_device(tbg_engine *engine, void *host, const void *d_src, uint64_t 
  * range of its batches (it writes their replies):
  *   1. tbg_shard_prepare_window: one pass over the window; the owners validate and resolve what they
  *      own (accounts, transfer ids) and write tbg_shard_exchange_bytes(operation, E, G) bytes of owner
- *      facts at d_exchange (a 16 B trailer of this shard's verdicts, then 2 B per create_transfers
- *      event plus G x 4096 ledger-mismatch slots of 8 B / 1 B per create_accounts event);
+ *      facts at d_exchange: a 16 B trailer (two alternating verdict words), fixed-size counters (per
+ *      shard its store room, 64 owned-id slots, 4096 ledger-mismatch slots of 8 B), then 2 B per
+ *      create_transfers event / 1 B per create_accounts event (csrc/shard.h xch_view). d_exchange
+ *      must be ONE buffer per shard, zeroed once at allocation and reused for every window: each
+ *      window zeroes the counters and the other verdict word for the next one (tbg_reset / tbg_open
+ *      restart the alternation on every shard alike);
  *   2. the caller sums those bytes element-wise across all G shards in place, ordered on the engine
  *      stream (ncclAllReduce(uint8, ncclSum) over xGMI, e.g. torch.distributed.all_reduce); every bit
  *      has exactly one writer, so the byte-wise sum is exact;

@@ -51,15 +51,19 @@ def _stream(seed, n_acc, n_batches):
     again["user_data_64"] = rng.integers(0, 2, BM)
     out.append(("a", again))
     next_id = win_start = 1
+    used = set()
     for k_batch in range(n_batches):
         if k_batch % WINDOW_BATCHES == 0:
             win_start = next_id  # retries only of ids from earlier windows: no in-window duplicates
+            used = set()         # (nor one earlier id retried twice in a window)
         n = int(rng.integers(1, BM + 1))
         t = np.zeros(n, TRANSFER_DTYPE)
         t["id_lo"] = np.arange(next_id, next_id + n, dtype=np.uint64)
         if win_start > 200:
             k = min(n // 6, 10)
-            t["id_lo"][:k] = rng.choice(np.arange(1, win_start - 1, dtype=np.uint64), k, replace=False)
+            pool = np.array(sorted(set(range(1, win_start - 1)) - used), dtype=np.uint64)
+            t["id_lo"][:k] = rng.choice(pool, k, replace=False)
+            used.update(int(x) for x in t["id_lo"][:k])
         next_id += n
         dr = rng.integers(1, n_acc + 5, n)
         cr = rng.integers(1, n_acc + 5, n)
