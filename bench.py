@@ -448,7 +448,8 @@ def run_sharded(args, torch, dist, world, rank, device):
     (tigerbeetle_amd/sharding.py, csrc/route.h): each rank generates and holds only its home batches of
     every window (1/N of the stream) and the three per-window all-to-alls carry the rest over RCCL."""
     from tigerbeetle_amd import _lib
-    from tigerbeetle_amd.sharding import ShardedStateMachine, alltoall_gloo, alltoall_nccl, route_bounds
+    from tigerbeetle_amd.sharding import (ShardedStateMachine, alltoall_gloo, alltoall_nccl, exchange_gloo,
+                                          exchange_nccl, route_bounds)
     from tigerbeetle_amd.state_machine import to_host
     from tigerbeetle_amd.types import Operation
 
@@ -465,9 +466,11 @@ def run_sharded(args, torch, dist, world, rank, device):
     n_batches = total_batches
     acc_cap = int(n_acc / G * 1.02) + 65536
     x_cap = int(n_xfer / G * 1.02) + win * BATCH
-    sm = ShardedStateMachine(G, me, None, device=device, batch_max=BATCH, accounts_max=acc_cap,
-                             transfers_max=x_cap, window_events_max=win * BATCH)
-    sm.alltoall = alltoall_gloo if args.backend == "gloo" else alltoall_nccl
+    gloo = args.backend == "gloo"
+    # (the all-reduce serves the general path: the harness pulses; the all-to-alls the routed windows)
+    sm = ShardedStateMachine(G, me, exchange_gloo if gloo else exchange_nccl, device=device, batch_max=BATCH,
+                             accounts_max=acc_cap, transfers_max=x_cap, window_events_max=WINDOW_BATCHES_MAX * BATCH)
+    sm.alltoall = alltoall_gloo if gloo else alltoall_nccl
     stream = sm.sm.stream
 
     def home_slices(n_total):
@@ -489,7 +492,7 @@ def run_sharded(args, torch, dist, world, rank, device):
     x_sl, n_x_home = home_slices(n_xfer)
     d_acc = torch.empty(max(n_acc_home, 1) * 128, dtype=torch.uint8, device="cuda")
     d_xfer = torch.empty(max(n_x_home, 1) * 128, dtype=torch.uint8, device="cuda")
-    d_res = torch.empty(win * BATCH * 8, dtype=torch.uint8, device="cuda")
+    d_res = torch.empty(WINDOW_BATCHES_MAX * BATCH * 8, dtype=torch.uint8, device="cuda")
     n_windows_max = max(len(acc_sl), len(x_sl)) + 1
     d_base = torch.zeros(n_windows_max * (WINDOW_BATCHES_MAX + 1), dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
@@ -517,6 +520,8 @@ def run_sharded(args, torch, dist, world, rank, device):
             prepare_ts += 1 + n
             ns.append(n)
             ts.append(prepare_ts)
+        if sm.pulse(ts[0]):  # the harness pulse before the window (general path; then never due again)
+            sm.commit_pulse(ts[0])
         _, count = sm.commit_window_routed(op, d_home.data_ptr() + off * 128, ns, ts, d_res.data_ptr(),
                                            d_base.data_ptr() + widx * (WINDOW_BATCHES_MAX + 1) * 4, bounds)
         return widx, count  # this rank's home batches: d_base[widx, count] = their failures

@@ -1,5 +1,7 @@
-"""Hash-sharded engine across processes: two ranks (one engine each, sharing cuda:0), both exchanges a
-real torch.distributed all-reduce (gloo through pinned host memory here; RCCL on a multi-GPU node).
+"""Hash-sharded engine across processes: two ranks (one engine each, sharing cuda:0), the exchanges real
+torch.distributed collectives (gloo through pinned host memory here; RCCL on a multi-GPU node): the
+replicated protocol's all-reduce, or the routed protocol's all-to-alls with each rank holding only its
+home batches.
 The ranks' replies (each for its home batches) and the union of their stores must equal the CPU
 restatement's."""
 import os
@@ -47,7 +49,7 @@ def _pack(replies):
     return b"".join(b"".join(len(x).to_bytes(4, "little") + x for x in w) + b"|" for w in replies)
 
 
-def _rank_main(rank, world, port, seed, n_acc, n_windows, out_dir):
+def _rank_main(rank, world, port, seed, n_acc, n_windows, out_dir, protocol="replicated"):
     import torch
     import torch.distributed as dist
 
@@ -56,12 +58,13 @@ def _rank_main(rank, world, port, seed, n_acc, n_windows, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from test_gpu_shard import LocalShards  # noqa: F401  (same harness timestamps)
 
-    from tigerbeetle_amd.sharding import ShardedStateMachine, exchange_gloo
+    from tigerbeetle_amd.sharding import ShardedStateMachine, alltoall_gloo, exchange_gloo, route_bounds
     from tigerbeetle_amd.state_machine import to_host
     from tigerbeetle_amd.types import Operation
 
     sh = ShardedStateMachine(world, rank, exchange_gloo, batch_max=BM, accounts_max=n_acc,
                              transfers_max=1 << 16, window_events_max=WIN * BM)
+    sh.alltoall = alltoall_gloo
     prepare_ts, replies = 0, []
     for kind, batches in _stream(seed, n_acc, n_windows):
         op = Operation.create_accounts if kind == "a" else Operation.create_transfers
@@ -70,12 +73,24 @@ def _rank_main(rank, world, port, seed, n_acc, n_windows, out_dir):
             prepare_ts += 1 + len(ev)
             ns.append(len(ev))
             ts.append(prepare_ts)
-        data = np.concatenate([np.frombuffer(ev.tobytes(), np.uint8) for ev in batches])
+        if protocol == "routed":  # partitioned ingestion: this rank holds only its home batches
+            bounds = route_bounds(len(ns), world)
+            part = batches[bounds[rank]: bounds[rank + 1]]
+        else:
+            part = batches
+        data = (np.concatenate([np.frombuffer(ev.tobytes(), np.uint8) for ev in part]) if part else
+                np.zeros(128, np.uint8))
         d_ev = torch.from_numpy(data.copy()).cuda()
-        d_res = torch.zeros(sum(ns) * 8, dtype=torch.uint8, device="cuda")
+        d_res = torch.zeros(max(sum(ns), 1) * 8, dtype=torch.uint8, device="cuda")
         d_base = torch.zeros(len(ns) + 1, dtype=torch.int32, device="cuda")
         torch.cuda.synchronize()
-        first, count = sh.commit_window(op, d_ev.data_ptr(), ns, ts, d_res.data_ptr(), d_base.data_ptr())
+        if protocol == "routed":
+            if sh.pulse(ts[0]):
+                sh.commit_pulse(ts[0])
+            first, count = sh.commit_window_routed(op, d_ev.data_ptr(), ns, ts, d_res.data_ptr(), d_base.data_ptr(),
+                                                   bounds)
+        else:
+            first, count = sh.commit_window(op, d_ev.data_ptr(), ns, ts, d_res.data_ptr(), d_base.data_ptr())
         sh.sync()
         res, base = to_host(d_res).tobytes(), to_host(d_base)
         replies.append([first] + [res[base[k] * 8: base[k + 1] * 8] for k in range(count)])
@@ -90,7 +105,8 @@ def _rank_main(rank, world, port, seed, n_acc, n_windows, out_dir):
 
 
 @pytest.mark.gpu
-def test_two_rank_gloo_matches_oracle(tmp_path):
+@pytest.mark.parametrize("protocol", ["replicated", "routed"])
+def test_two_rank_gloo_matches_oracle(tmp_path, protocol):
     import torch.multiprocessing as mp
 
     from oracle_sm import OracleStateMachine
@@ -98,7 +114,8 @@ def test_two_rank_gloo_matches_oracle(tmp_path):
     from tigerbeetle_amd.types import Operation
 
     world, seed, n_acc, n_windows = 2, 5, 600, 6
-    mp.spawn(_rank_main, args=(world, _free_port(), seed, n_acc, n_windows, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank_main, args=(world, _free_port(), seed, n_acc, n_windows, str(tmp_path), protocol), nprocs=world,
+             join=True)
     ref = OracleStateMachine(batch_max=BM)
     try:
         expect = []

@@ -224,6 +224,10 @@ def main():
             prepare_ts += 1 + n
             ns.append(n)
             ts.append(prepare_ts)
+        if shards[0].pulse(ts[0]):  # the harness pulse before the window (the first one only here)
+            from tigerbeetle_amd.sharding import pulse_general
+
+            pulse_general(shards, summed, ts[0])
         bounds = route_bounds(len(ns), G)
         homes = [d_ev.data_ptr() + (b0 + bounds[r]) * BATCH * 128 for r in range(G)]
         _, ev1 = timed_step(lambda r, s: s.route_prepare(op, homes[r], ns, ts, bounds))
