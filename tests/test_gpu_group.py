@@ -27,13 +27,13 @@ def _compare_final(gpu, ref):
     assert np.array_equal(gpu.dump_transfer_status(), ref.dump_transfer_status())
 
 
-def _lookups(gpu, ref, rng):
+def _lookups(gpu, ref, rng, batch_max):
     acc = ref.dump_accounts()
     xf = ref.dump_transfers()
     for op, recs in ((Operation.lookup_accounts, acc), (Operation.lookup_transfers, xf)):
         if not len(recs):
             continue
-        k = rng.choice(len(recs), min(40, len(recs)), replace=False)
+        k = rng.choice(len(recs), min(40, len(recs), batch_max - 3), replace=False)  # (input_valid: <= batch_max)
         ids = np.zeros((len(k) + 3, 2), np.uint64)
         ids[: len(k), 0], ids[: len(k), 1] = recs["id_lo"][k], recs["id_hi"][k]
         ids[len(k):, 0] = [987654321, 0, 5]  # missing ids, a zero id
@@ -59,7 +59,7 @@ def _chaos_group(G, seed, batches, batch_max, tick_every=3, **kw):
             # the next pulse() decision (state_machine.zig:589-596) reads this value
             assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp(), f"G {G} seed {seed} batch {b}"
         _compare_final(gpu, ref)
-        _lookups(gpu, ref, np.random.default_rng(seed))
+        _lookups(gpu, ref, np.random.default_rng(seed), batch_max)
     finally:
         gpu.close()
         ref.close()

@@ -148,7 +148,10 @@ struct RtBufs {
   unsigned long long* claim;  // owner: in-window duplicate ids, {epoch, flat id message}
   uint32_t claim_mask;
   unsigned long long* amt;  // owner: 64 slots x {low 32 bits, the rest} of the received amounts' sum
-  uint32_t* hv;             // [0] the home verdict (k_rt_scan -> k_rt_decide)
+  uint32_t* hv;             // [0] the home verdict (k_rt_scan -> k_rt_decide); k_rt_prefix -> k_rt_apply:
+                            // [1] every owned balance field stays below 2^64, [2] the global verdict,
+                            // [3] committed records in all
+  uint32_t* cbase;          // k_rt_prefix: per (source, 1024-message chunk), the committed records before it
 };
 
 __device__ inline uint32_t rt_lane_lt(unsigned long long m) {
@@ -684,6 +687,47 @@ __host__ __device__ inline uint32_t rt_apply_blocks(const RtLayout& L, uint32_t 
   return nh + a + b;
 }
 
+// k_rt_prefix (one workgroup, after exchange C): what every k_rt_apply block would otherwise fold from
+// the G C headers itself: the verdict, the committed records' exclusive base per (source, chunk) in
+// (source, chunk) order, their total, and whether this window's adds stay below 2^64 on this owner.
+__global__ void __launch_bounds__(1024) k_rt_prefix(Dev d, RtBufs rb, RtLayout L) {
+  __shared__ uint32_t carry, vsh;
+  const uint32_t G = L.G, lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) {
+    carry = 0;
+    vsh = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x < G) atomicOr(&vsh, *reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, threadIdx.x)));
+  uint32_t flat = 0;
+  for (uint32_t sg = 0; sg < G; sg++) {
+    const uint32_t nch = rt_nch(L.c1[sg]);
+    const uint32_t* cnt = reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, sg) + RT_HDR_C);
+    // one wave scans (the counts are few: ~n / (G x 1024) per source)
+    if (threadIdx.x < 64)
+      for (uint32_t q0 = 0; q0 < nch; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const uint32_t v = q < nch ? cnt[q] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        if (q < nch) rb.cbase[flat + q] = carry + inc - v;
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        wave_sync();
+        if (lane == 0) carry += tot;
+        wave_sync();
+      }
+    flat += nch;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u128 tot = 0;
+    for (int q = 0; q < 64; q++) tot += (u128)rb.amt[q * 2] + ((u128)rb.amt[q * 2 + 1] << 32);
+    const u128 top = d.g->ovf_bound + tot;
+    rb.hv[1] = (top >= d.g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1u : 0u;
+    rb.hv[2] = vsh;
+    rb.hv[3] = carry;
+  }
+}
+
 template <bool XFER>
 __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, WinDesc w, RtLayout L, uint32_t nh,
                                                    FinalOut o, ChgLog chg, uint32_t chg_epoch) {
@@ -694,15 +738,8 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   Globals* g = d.g;
   const uint32_t G = L.G;
   if (threadIdx.x == 0) {
-    uint32_t v = 0, total = 0;
-    for (uint32_t sg = 0; sg < G; sg++) {
-      const uint8_t* c = rb.c_recv + rt_off_c(L, sg);
-      v |= *reinterpret_cast<const uint32_t*>(c);
-      const uint32_t* cnt = reinterpret_cast<const uint32_t*>(c + RT_HDR_C);
-      for (uint32_t q = 0; q < rt_nch(L.c1[sg]); q++) total += cnt[q];
-    }
-    sh_v = v;
-    sh_total = total;
+    sh_v = rb.hv[2];      // (k_rt_prefix)
+    sh_total = rb.hv[3];
     uint32_t b = blockIdx.x, role = 0, sg = 0, k0 = 0;
     if (b >= nh) {
       b -= nh;
@@ -715,19 +752,14 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
       k0 = b * RT_T;
       if (sg == G) {
         role = 2;
-        uint32_t base = 0;
+        const uint32_t flat = b;  // (the id blocks are the chunks in (source, chunk) order)
         for (sg = 0; sg < G; sg++) {
           const uint32_t nb = rt_nch(L.c1[sg]);
-          const uint32_t* cnt = reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, sg) + RT_HDR_C);
-          if (b < nb) {
-            for (uint32_t q = 0; q < b; q++) base += cnt[q];
-            break;
-          }
-          for (uint32_t q = 0; q < nb; q++) base += cnt[q];
+          if (b < nb) break;
           b -= nb;
         }
         k0 = b * RT_CHUNK;
-        sh_base = base;
+        sh_base = sg < G ? rb.cbase[flat] : 0u;
       }
     }
     sh_role = role;
@@ -735,13 +767,8 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     sh_k0 = k0;
     const RtHdrA* h = sg < G ? reinterpret_cast<const RtHdrA*>(rb.a_recv + rt_off_a(L, sg)) : nullptr;
     sh_n = h ? (role == 1 ? h->n_side : h->n_id) : 0u;
-    if (role == 1 && XFER) {
-      // every balance field stays below 2^64 this window: ovf_bound + the received amounts' sum
-      u128 tot = 0;
-      for (int q = 0; q < 64; q++) tot += (u128)rb.amt[q * 2] + ((u128)rb.amt[q * 2 + 1] << 32);
-      const u128 top = g->ovf_bound + tot;
-      sh_small = (top >= g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1ull : 0ull;
-    }
+    // every balance field stays below 2^64 this window: ovf_bound + the received amounts' sum (k_rt_prefix)
+    if (role == 1 && XFER) sh_small = rb.hv[1];
   }
   __syncthreads();
   if (sh_v) {
