@@ -39,7 +39,8 @@
 #include "shard.h"
 
 #define RT_MAXG 16
-#define RT_T 1024       // home kernels' block (route, apply); k_rt_own / k_rt_decide use 256
+#define RT_T 1024       // k_rt_apply's block (= SEG: the home replies' segments); k_rt_own / k_rt_decide use 256
+#define RT_RT 256       // k_rt_route1 / k_rt_route2's block (small blocks: a shard's slice fills the chip)
 #define RT_CHUNK 1024   // committed-record counts per chunk of id messages (one k_rt_apply block each)
 #define RT_HDR_A 256u   // bytes
 #define RT_HDR_B 64u
@@ -189,16 +190,16 @@ __device__ inline bool rt_claim(unsigned long long* map, uint32_t mask, uint32_t
 enum : uint32_t { RC_REACH = 1u << 12, RC_LINKED = 1u << 13 };
 
 template <bool XFER>
-__global__ void __launch_bounds__(RT_T) k_rt_route1(Dev d, Scratch s, RtBufs rb, const uint8_t* __restrict__ ev_bytes,
-                                                    WinDesc w, RtLayout L) {
+__global__ void __launch_bounds__(RT_RT) k_rt_route1(Dev d, Scratch s, RtBufs rb, const uint8_t* __restrict__ ev_bytes,
+                                                     WinDesc w, RtLayout L) {
   __shared__ uint32_t lcnt[RT_MAXG * 2];
   __shared__ uint32_t laux;
-  const uint32_t i = blockIdx.x * RT_T + threadIdx.x;
+  const uint32_t i = blockIdx.x * RT_RT + threadIdx.x;
   const uint32_t G = L.G;
   if (threadIdx.x < RT_MAXG * 2) lcnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) {
     laux = 0;
-    s.cnt_bad[blockIdx.x] = 0;  // this segment's failures (k_rt_decide adds to them; RT_T == SEG)
+    if ((i & (SEG - 1)) == 0) s.cnt_bad[i / SEG] = 0;  // this segment's failures (k_rt_decide adds to them)
   }
   __syncthreads();
   bool reach = false;
@@ -323,10 +324,10 @@ __global__ void __launch_bounds__(1024) k_rt_scan(Dev d, RtBufs rb, const uint8_
 // ranks by ballot). Scratch amt (as uint4): {id message rank, debit side rank, credit side rank}.
 // ------------------------------------------------------------------------------------------------
 template <bool XFER>
-__global__ void __launch_bounds__(RT_T) k_rt_route2(Dev d, Scratch s, RtBufs rb, const uint8_t* __restrict__ ev_bytes,
-                                                    WinDesc w, RtLayout L) {
-  __shared__ uint32_t wcnt[RT_T / 64][RT_MAXG * 2];
-  const uint32_t i = blockIdx.x * RT_T + threadIdx.x;
+__global__ void __launch_bounds__(RT_RT) k_rt_route2(Dev d, Scratch s, RtBufs rb, const uint8_t* __restrict__ ev_bytes,
+                                                     WinDesc w, RtLayout L) {
+  __shared__ uint32_t wcnt[RT_RT / 64][RT_MAXG * 2];
+  const uint32_t i = blockIdx.x * RT_RT + threadIdx.x;
   const uint32_t G = L.G, me = L.me, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t cls = i < w.E ? s.cls[i] : 0u;
   const bool reach = (cls & RC_REACH) != 0;
