@@ -149,10 +149,7 @@ struct RtBufs {
   unsigned long long* claim;  // owner: in-window duplicate ids, {epoch, flat id message}
   uint32_t claim_mask;
   unsigned long long* amt;  // owner: 64 slots x {low 32 bits, the rest} of the received amounts' sum
-  uint32_t* hv;             // [0] the home verdict (k_rt_scan -> k_rt_decide); k_rt_prefix -> k_rt_apply:
-                            // [1] every owned balance field stays below 2^64, [2] the global verdict,
-                            // [3] committed records in all
-  uint32_t* cbase;          // k_rt_prefix: per (source, 1024-message chunk), the committed records before it
+  uint32_t* hv;             // [0] the home verdict (k_rt_scan -> k_rt_decide)
 };
 
 __device__ inline uint32_t rt_lane_lt(unsigned long long m) {
@@ -259,22 +256,39 @@ __global__ void __launch_bounds__(1024) k_rt_scan(Dev d, RtBufs rb, const uint8_
                                                   uint32_t nblk, RtLayout L, uint64_t t_last, uint64_t first_ts,
                                                   uint32_t multi) {
   __shared__ uint32_t tot[RT_MAXG * 2];
+  __shared__ uint32_t seg[1024];  // per (column, segment): the segment's sum, then its exclusive base
   __shared__ uint32_t vbits;
-  const uint32_t G = L.G, me = L.me;
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t G = L.G, me = L.me, ncol = 2 * G;
   if (threadIdx.x == 0) vbits = 0;
+  // thread t: column t % ncol, segment t / ncol of the route blocks (every load independent: no serial
+  // chain of global latencies through one wave)
+  const uint32_t nseg = 1024 / ncol, col = threadIdx.x % ncol, sg = threadIdx.x / ncol;
+  const uint32_t per = (nblk + nseg - 1) / nseg;
+  const uint32_t b0 = sg * per, b1 = min(nblk, b0 + per);
+  const bool on = sg < nseg;
+  uint32_t sum = 0;
+  if (on)
+    for (uint32_t b = b0; b < b1; b++) sum += rb.cnt[(size_t)b * RT_MAXG * 2 + col];
+  seg[threadIdx.x] = sum;
   __syncthreads();
-  // one wave per column (destination x kind)
-  for (uint32_t col = wave; col < 2 * G; col += 16) {
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < nblk; b0 += 64) {
-      const uint32_t b = b0 + lane;
-      const uint32_t v = b < nblk ? rb.cnt[(size_t)b * RT_MAXG * 2 + col] : 0u;
-      const uint32_t inc = wave_incl_scan(v);
-      if (b < nblk) rb.boff[(size_t)b * RT_MAXG * 2 + col] = carry + inc - v;
-      carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+  if (threadIdx.x < ncol) {  // per column: the segments' exclusive bases and the total
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < nseg; k++) {
+      const uint32_t v = seg[k * ncol + threadIdx.x];
+      seg[k * ncol + threadIdx.x] = c;
+      c += v;
     }
-    if (lane == 0) tot[col] = carry;
+    tot[threadIdx.x] = c;
+  }
+  __syncthreads();
+  if (on) {
+    uint32_t c = seg[threadIdx.x];
+    for (uint32_t b = b0; b < b1; b++) {
+      const size_t k = (size_t)b * RT_MAXG * 2 + col;
+      const uint32_t v = rb.cnt[k];
+      rb.boff[k] = c;
+      c += v;
+    }
   }
   uint32_t a = 0;
   for (uint32_t b = threadIdx.x; b < nblk; b += 1024) a |= rb.aux[b];
@@ -688,47 +702,6 @@ __host__ __device__ inline uint32_t rt_apply_blocks(const RtLayout& L, uint32_t 
   return nh + a + b;
 }
 
-// k_rt_prefix (one workgroup, after exchange C): what every k_rt_apply block would otherwise fold from
-// the G C headers itself: the verdict, the committed records' exclusive base per (source, chunk) in
-// (source, chunk) order, their total, and whether this window's adds stay below 2^64 on this owner.
-__global__ void __launch_bounds__(1024) k_rt_prefix(Dev d, RtBufs rb, RtLayout L) {
-  __shared__ uint32_t carry, vsh;
-  const uint32_t G = L.G, lane = threadIdx.x & 63;
-  if (threadIdx.x == 0) {
-    carry = 0;
-    vsh = 0;
-  }
-  __syncthreads();
-  if (threadIdx.x < G) atomicOr(&vsh, *reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, threadIdx.x)));
-  uint32_t flat = 0;
-  for (uint32_t sg = 0; sg < G; sg++) {
-    const uint32_t nch = rt_nch(L.c1[sg]);
-    const uint32_t* cnt = reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, sg) + RT_HDR_C);
-    // one wave scans (the counts are few: ~n / (G x 1024) per source)
-    if (threadIdx.x < 64)
-      for (uint32_t q0 = 0; q0 < nch; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        const uint32_t v = q < nch ? cnt[q] : 0u;
-        const uint32_t inc = wave_incl_scan(v);
-        if (q < nch) rb.cbase[flat + q] = carry + inc - v;
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        wave_sync();
-        if (lane == 0) carry += tot;
-        wave_sync();
-      }
-    flat += nch;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    u128 tot = 0;
-    for (int q = 0; q < 64; q++) tot += (u128)rb.amt[q * 2] + ((u128)rb.amt[q * 2 + 1] << 32);
-    const u128 top = d.g->ovf_bound + tot;
-    rb.hv[1] = (top >= d.g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1u : 0u;
-    rb.hv[2] = vsh;
-    rb.hv[3] = carry;
-  }
-}
-
 template <bool XFER>
 __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, WinDesc w, RtLayout L, uint32_t nh,
                                                    FinalOut o, ChgLog chg, uint32_t chg_epoch) {
@@ -739,8 +712,6 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   Globals* g = d.g;
   const uint32_t G = L.G;
   if (threadIdx.x == 0) {
-    sh_v = rb.hv[2];      // (k_rt_prefix)
-    sh_total = rb.hv[3];
     uint32_t b = blockIdx.x, role = 0, sg = 0, k0 = 0;
     if (b >= nh) {
       b -= nh;
@@ -753,14 +724,13 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
       k0 = b * RT_T;
       if (sg == G) {
         role = 2;
-        const uint32_t flat = b;  // (the id blocks are the chunks in (source, chunk) order)
+        sh_base = b;  // (the id blocks are the chunks in (source, chunk) order: this one's flat index)
         for (sg = 0; sg < G; sg++) {
           const uint32_t nb = rt_nch(L.c1[sg]);
           if (b < nb) break;
           b -= nb;
         }
         k0 = b * RT_CHUNK;
-        sh_base = sg < G ? rb.cbase[flat] : 0u;
       }
     }
     sh_role = role;
@@ -768,8 +738,56 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     sh_k0 = k0;
     const RtHdrA* h = sg < G ? reinterpret_cast<const RtHdrA*>(rb.a_recv + rt_off_a(L, sg)) : nullptr;
     sh_n = h ? (role == 1 ? h->n_side : h->n_id) : 0u;
-    // every balance field stays below 2^64 this window: ovf_bound + the received amounts' sum (k_rt_prefix)
-    if (role == 1 && XFER) sh_small = rb.hv[1];
+  }
+  // what every block folds from the G C headers, in parallel: the verdict; the committed records in all
+  // and, for an id block, before its chunk ((source, chunk) order); for a side block, whether the
+  // received amounts keep every balance field below 2^64
+  __shared__ uint32_t f_v;
+  __shared__ unsigned long long f_amt[2];
+  if (threadIdx.x == 0) {
+    f_v = 0;
+    f_amt[0] = f_amt[1] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x < G) atomicOr(&f_v, *reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, threadIdx.x)));
+  const uint32_t my_flat = sh_role == 2 ? sh_base : 0u;
+  uint32_t before = 0, all = 0;
+  {
+    uint32_t flat0 = 0;
+    for (uint32_t s2 = 0; s2 < G; s2++) {
+      const uint32_t nch = rt_nch(L.c1[s2]);
+      const uint32_t* cnt = reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, s2) + RT_HDR_C);
+      for (uint32_t q = threadIdx.x; q < nch; q += RT_T) {
+        const uint32_t v = cnt[q];
+        all += v;
+        if (flat0 + q < my_flat) before += v;
+      }
+      flat0 += nch;
+    }
+  }
+  if (XFER && sh_role == 1 && threadIdx.x < 64) {
+    unsigned long long lo = rb.amt[threadIdx.x * 2], hi = rb.amt[threadIdx.x * 2 + 1];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo += __shfl_xor(lo, o, 64);
+      hi += __shfl_xor(hi, o, 64);
+    }
+    if (threadIdx.x == 0) {
+      f_amt[0] = lo;
+      f_amt[1] = hi;
+    }
+  }
+  all = block_sum<RT_T / 64>(all, lds);
+  before = block_sum<RT_T / 64>(before, lds);
+  if (threadIdx.x == 0) {
+    sh_v = f_v;
+    sh_total = all;
+    if (sh_role == 2) sh_base = before;
+    if (XFER && sh_role == 1) {
+      const u128 tot = (u128)f_amt[0] + ((u128)f_amt[1] << 32);
+      const u128 top = g->ovf_bound + tot;
+      sh_small = (top >= g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1ull : 0ull;
+    }
   }
   __syncthreads();
   if (sh_v) {
