@@ -267,22 +267,30 @@ __global__ void __launch_bounds__(1024) k_rt_scan(Dev d, RtBufs rb, const uint8_
   const uint32_t b0 = sg * per, b1 = min(nblk, b0 + per);
   const bool on = sg < nseg;
   uint32_t sum = 0;
-  if (on)
+  if (on) {
+#pragma unroll 8
     for (uint32_t b = b0; b < b1; b++) sum += rb.cnt[(size_t)b * RT_MAXG * 2 + col];
+  }
   seg[threadIdx.x] = sum;
   __syncthreads();
-  if (threadIdx.x < ncol) {  // per column: the segments' exclusive bases and the total
-    uint32_t c = 0;
-    for (uint32_t k = 0; k < nseg; k++) {
-      const uint32_t v = seg[k * ncol + threadIdx.x];
-      seg[k * ncol + threadIdx.x] = c;
-      c += v;
+  {  // per column, one wave: the segments' exclusive bases (wave scans, 64 segments a step) and the total
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    for (uint32_t c = wv; c < ncol; c += 1024 / 64) {
+      uint32_t carry = 0;
+      for (uint32_t k0 = 0; k0 < nseg; k0 += 64) {
+        const uint32_t k = k0 + ln;
+        const uint32_t v = k < nseg ? seg[k * ncol + c] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        if (k < nseg) seg[k * ncol + c] = carry + inc - v;
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+      }
+      if (ln == 0) tot[c] = carry;
     }
-    tot[threadIdx.x] = c;
   }
   __syncthreads();
   if (on) {
     uint32_t c = seg[threadIdx.x];
+#pragma unroll 8
     for (uint32_t b = b0; b < b1; b++) {
       const size_t k = (size_t)b * RT_MAXG * 2 + col;
       const uint32_t v = rb.cnt[k];
@@ -405,25 +413,58 @@ __global__ void __launch_bounds__(RT_RT) k_rt_route2(Dev d, Scratch s, RtBufs rb
 }
 
 // The global facts every shard derives identically from the G A headers it received: the window's ids
-// strictly increasing across the slices (rank order = event order), and the first id.
-__device__ inline bool rt_global_mono(const uint8_t* a_recv, const RtLayout& L, tb_uint128_t* first) {
-  bool mono = true, any = false;
-  u128 last = 0;
-  first->lo = first->hi = 0;
-  for (uint32_t sg = 0; sg < L.G; sg++) {
-    const RtHdrA* h = reinterpret_cast<const RtHdrA*>(a_recv + rt_off_a(L, sg));
-    if (!(h->flags & RH_NONEMPTY)) continue;
-    if (h->flags & RH_NONMONO) mono = false;
-    const u128 f = ((u128)h->first_hi << 64) | h->first_lo, l = ((u128)h->last_hi << 64) | h->last_lo;
-    if (any && !(f > last)) mono = false;
-    if (!any) {
-      first->lo = h->first_lo;
-      first->hi = h->first_hi;
-    }
-    any = true;
-    last = l;
+// strictly increasing across the slices (rank order = event order), the first id, the message counts.
+// One wave: lane l < G reads header l (all G loads in flight at once; a serial walk over the headers
+// put G dependent global latencies in front of every block). Every lane of the wave calls it; `pick`
+// (wave-uniform) selects the header whose own counts come back in n_id / n_side (0 past G).
+struct RtAFold {
+  bool mono;
+  tb_uint128_t first;
+  uint32_t n_id, n_side;        // header `pick`
+  unsigned long long nid, nside;  // over all G headers
+};
+__device__ inline RtAFold rt_fold_a(const uint8_t* a_recv, const RtLayout& L, uint32_t pick) {
+  const uint32_t l = threadIdx.x & 63;
+  uint32_t flags = 0, nid = 0, nside = 0;
+  unsigned long long f0 = 0, f1 = 0, l0 = 0, l1 = 0;
+  if (l < L.G) {
+    const RtHdrA* h = reinterpret_cast<const RtHdrA*>(a_recv + rt_off_a(L, l));
+    flags = h->flags;
+    nid = h->n_id;
+    nside = h->n_side;
+    f0 = h->first_lo;
+    f1 = h->first_hi;
+    l0 = h->last_lo;
+    l1 = h->last_hi;
   }
-  return mono;
+  const bool ne = (flags & RH_NONEMPTY) != 0;
+  const unsigned long long mne = __ballot(ne);
+  const unsigned long long below = mne & ((1ull << l) - 1ull);
+  const int prev = below ? 63 - __builtin_clzll(below) : -1;  // the previous non-empty slice
+  const int src = prev < 0 ? (int)l : prev;
+  const unsigned long long p0 = __shfl(l0, src, 64), p1 = __shfl(l1, src, 64);
+  bool bad = false;
+  if (ne) {
+    if (flags & RH_NONMONO) bad = true;
+    if (prev >= 0 && !((((u128)f1 << 64) | f0) > (((u128)p1 << 64) | p0))) bad = true;
+  }
+  RtAFold r;
+  r.mono = __ballot(bad) == 0;
+  const int fl = mne ? __builtin_ctzll(mne) : 0;
+  const unsigned long long g0 = __shfl(f0, fl, 64), g1 = __shfl(f1, fl, 64);
+  r.first.lo = mne ? g0 : 0;
+  r.first.hi = mne ? g1 : 0;
+  r.n_id = (uint32_t)__shfl((int)nid, (int)pick, 64);
+  r.n_side = (uint32_t)__shfl((int)nside, (int)pick, 64);
+  unsigned long long a = nid, b = nside;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  r.nid = a;
+  r.nside = b;
+  return r;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -443,61 +484,53 @@ __host__ __device__ inline uint32_t rt_own_blocks(const RtLayout& L, uint32_t* i
 
 template <bool XFER>
 __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout L, uint32_t epoch) {
-  __shared__ uint32_t sh_src, sh_k0, sh_n, sh_side, sh_claim;
+  __shared__ uint32_t sh_n, sh_claim;
   __shared__ unsigned long long ared[RT_OWN_T / 64][2];
   Globals* g = d.g;
   const uint32_t G = L.G;
-  if (threadIdx.x == 0) {
-    // this block's source shard and first message
-    uint32_t b = blockIdx.x, side = 0, sg = 0;
-    uint32_t nb = 0;
-    for (; sg < G; sg++) {
-      nb = (L.c1[sg] + RT_OWN_T - 1) / RT_OWN_T;
+  // this block's source shard and first message (kernel arguments only: the same in every thread)
+  uint32_t b = blockIdx.x, side = 0, sg = 0;
+  for (; sg < G; sg++) {
+    const uint32_t nb = (L.c1[sg] + RT_OWN_T - 1) / RT_OWN_T;
+    if (b < nb) break;
+    b -= nb;
+  }
+  if (sg == G) {
+    side = 1;
+    for (sg = 0; sg < G; sg++) {
+      const uint32_t nb = (L.c2[sg] + RT_OWN_T - 1) / RT_OWN_T;
       if (b < nb) break;
       b -= nb;
     }
-    if (sg == G) {
-      side = 1;
-      for (sg = 0; sg < G; sg++) {
-        nb = (L.c2[sg] + RT_OWN_T - 1) / RT_OWN_T;
-        if (b < nb) break;
-        b -= nb;
-      }
+  }
+  if (threadIdx.x < 64) {
+    const RtAFold f = rt_fold_a(rb.a_recv, L, sg);
+    if (threadIdx.x == 0) {
+      sh_n = side ? f.n_side : f.n_id;
+      sh_claim = (!XFER || !f.mono) ? 1u : 0u;
     }
-    sh_src = sg;
-    sh_side = side;
-    sh_k0 = b * RT_OWN_T;
-    const RtHdrA* h = sg < G ? reinterpret_cast<const RtHdrA*>(rb.a_recv + rt_off_a(L, sg)) : nullptr;
-    sh_n = h ? (side ? h->n_side : h->n_id) : 0u;
-    tb_uint128_t first;
-    const bool mono = rt_global_mono(rb.a_recv, L, &first);
-    sh_claim = (!XFER || !mono) ? 1u : 0u;
     if (blockIdx.x == 0) {
       // static verdicts of this owner (the same arithmetic wherever it runs): room, overflow bound
-      uint64_t nid = 0, nside = 0;
-      for (uint32_t s2 = 0; s2 < G; s2++) {
-        const RtHdrA* h2 = reinterpret_cast<const RtHdrA*>(rb.a_recv + rt_off_a(L, s2));
-        nid += h2->n_id;
-        nside += h2->n_side;
-      }
       uint32_t v = 0;
-      if (nid > (XFER ? d.x_max - g->x_count : d.acc_max - g->acc_count)) v |= RV_CAP;
-      if (XFER && nside && g->ovf_bound > MAX128 - ((u128)nside << 64)) v |= RV_OVF;
-      for (uint32_t hh = 0; hh < G; hh++) *reinterpret_cast<uint32_t*>(rb.b_send + rt_off_b(L, hh)) = v;
-      // the apply's insert base and whether the window extends this shard's sorted prefix (its records
-      // rise across the whole window and start above every id it stores)
-      g->base = XFER ? g->x_count : g->acc_count;
-      if (XFER) g->win_flags = (mono && nid && U(first) > g->x_id_max && g->x_sorted == g->x_count) ? 2u : 0u;
-      // (mono: the first message's id is the window's first; an owner whose first record comes later
-      // still sees it above: the ids rise)
+      if (f.nid > (XFER ? d.x_max - g->x_count : d.acc_max - g->acc_count)) v |= RV_CAP;
+      if (XFER && f.nside && g->ovf_bound > MAX128 - ((u128)f.nside << 64)) v |= RV_OVF;
+      if (threadIdx.x < G) *reinterpret_cast<uint32_t*>(rb.b_send + rt_off_b(L, threadIdx.x)) = v;
+      if (threadIdx.x == 0) {
+        // the apply's insert base and whether the window extends this shard's sorted prefix (its records
+        // rise across the whole window and start above every id it stores)
+        g->base = XFER ? g->x_count : g->acc_count;
+        if (XFER) g->win_flags = (f.mono && f.nid && U(f.first) > g->x_id_max && g->x_sorted == g->x_count) ? 2u : 0u;
+        // (mono: the first message's id is the window's first; an owner whose first record comes later
+        // still sees it above: the ids rise)
+      }
     }
   }
   __syncthreads();
-  const uint32_t sg = sh_src, k = sh_k0 + threadIdx.x;
   if (sg >= G) return;
+  const uint32_t k = b * RT_OWN_T + threadIdx.x;
   const bool live = k < sh_n;
   unsigned long long alo = 0, ahi = 0;
-  if (!sh_side) {
+  if (!side) {
     if (live) {
       const uint8_t* rec = rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)k * 128;
       uint32_t code;
@@ -606,13 +639,14 @@ __global__ void __launch_bounds__(RT_DEC_T) k_rt_decide(Dev d, Scratch s, RtBufs
   if (threadIdx.x == 0) {
     nbad = 0;
     vsh = 0;
-    if (blockIdx.x == 0) {
-      // the owners' verdicts (B headers) and this home's (k_rt_scan), into every C header
-      uint32_t v = rb.hv[0];
-      for (uint32_t o = 0; o < G; o++) v |= *reinterpret_cast<const uint32_t*>(rb.b_recv + o * rt_blk_b(L, me));
-      if (v)
-        for (uint32_t o = 0; o < G; o++) atomicOr(reinterpret_cast<uint32_t*>(rb.c_send + o * cb), v);
-    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    // the owners' verdicts (B headers, one lane each) and this home's (k_rt_scan), into every C header
+    uint32_t v = threadIdx.x < G ? *reinterpret_cast<const uint32_t*>(rb.b_recv + threadIdx.x * rt_blk_b(L, me)) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
+    v |= rb.hv[0];
+    if (v && threadIdx.x < G) atomicOr(reinterpret_cast<uint32_t*>(rb.c_send + threadIdx.x * cb), v);
   }
   __syncthreads();
   const uint32_t i = blockIdx.x * RT_DEC_T + threadIdx.x, seg = i / SEG;
@@ -680,11 +714,8 @@ __global__ void __launch_bounds__(RT_DEC_T) k_rt_decide(Dev d, Scratch s, RtBufs
   if ((threadIdx.x & 63) == 0 && wb) atomicAdd(&nbad, wb);
   if (verdict) atomicOr(&vsh, verdict);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    if (nbad) atomicAdd(&s.cnt_bad[seg], nbad);
-    if (vsh)
-      for (uint32_t o = 0; o < G; o++) atomicOr(reinterpret_cast<uint32_t*>(rb.c_send + o * cb), vsh);
-  }
+  if (threadIdx.x == 0 && nbad) atomicAdd(&s.cnt_bad[seg], nbad);
+  if (vsh && threadIdx.x < G) atomicOr(reinterpret_cast<uint32_t*>(rb.c_send + threadIdx.x * cb), vsh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -704,7 +735,10 @@ __host__ __device__ inline uint32_t rt_apply_blocks(const RtLayout& L, uint32_t 
 
 template <bool XFER>
 __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, WinDesc w, RtLayout L, uint32_t nh,
-                                                   FinalOut o, ChgLog chg, uint32_t chg_epoch) {
+                                                   FinalOut o, ChgLog chg, uint32_t chg_epoch, uint32_t b_off,
+                                                   uint32_t nblk) {
+  // (b_off / nblk: the grid may be launched in parts, one per role — TBG_RT_SPLIT, a profiling aid)
+  const uint32_t bid = blockIdx.x + b_off;
   __shared__ uint32_t lds[RT_T / 64];
   __shared__ uint32_t sh_v, sh_src, sh_k0, sh_n, sh_role, sh_base, sh_total;
   __shared__ unsigned long long sh_small;
@@ -712,7 +746,7 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   Globals* g = d.g;
   const uint32_t G = L.G;
   if (threadIdx.x == 0) {
-    uint32_t b = blockIdx.x, role = 0, sg = 0, k0 = 0;
+    uint32_t b = bid, role = 0, sg = 0, k0 = 0;
     if (b >= nh) {
       b -= nh;
       role = 1;
@@ -753,16 +787,38 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   const uint32_t my_flat = sh_role == 2 ? sh_base : 0u;
   uint32_t before = 0, all = 0;
   {
+    // one count per thread and source (a source has at most RT_T chunks unless its capacity passes 1M
+    // messages: the loop after takes the rest); the G loads are issued before any is used
+    uint32_t v[RT_MAXG], fl[RT_MAXG];
     uint32_t flat0 = 0;
-    for (uint32_t s2 = 0; s2 < G; s2++) {
-      const uint32_t nch = rt_nch(L.c1[s2]);
-      const uint32_t* cnt = reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, s2) + RT_HDR_C);
-      for (uint32_t q = threadIdx.x; q < nch; q += RT_T) {
-        const uint32_t v = cnt[q];
-        all += v;
-        if (flat0 + q < my_flat) before += v;
+    uint64_t off = 0;
+#pragma unroll
+    for (uint32_t s2 = 0; s2 < RT_MAXG; s2++) {
+      v[s2] = 0;
+      fl[s2] = flat0 + threadIdx.x;
+      if (s2 < G) {
+        const uint32_t nch = rt_nch(L.c1[s2]);
+        if (threadIdx.x < nch) v[s2] = reinterpret_cast<const uint32_t*>(rb.c_recv + off + RT_HDR_C)[threadIdx.x];
+        flat0 += nch;
+        off += rt_blk_c(L, s2);
       }
-      flat0 += nch;
+    }
+#pragma unroll
+    for (uint32_t s2 = 0; s2 < RT_MAXG; s2++) {
+      all += v[s2];
+      if (fl[s2] < my_flat) before += v[s2];
+    }
+    if (flat0 > RT_T) {
+      flat0 = 0;
+      for (uint32_t s2 = 0; s2 < G; s2++) {
+        const uint32_t nch = rt_nch(L.c1[s2]);
+        const uint32_t* cnt = reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, s2) + RT_HDR_C);
+        for (uint32_t q = threadIdx.x + RT_T; q < nch; q += RT_T) {
+          all += cnt[q];
+          if (flat0 + q < my_flat) before += cnt[q];
+        }
+        flat0 += nch;
+      }
     }
   }
   if (XFER && sh_role == 1 && threadIdx.x < 64) {
@@ -791,18 +847,18 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   }
   __syncthreads();
   if (sh_v) {
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) atomicOr(&g->window_error, 2u);
+    if (bid == nblk - 1 && threadIdx.x == 0) atomicOr(&g->window_error, 2u);
     return;
   }
   const uint32_t role = sh_role, sg = sh_src;
   if (role == 0) {
     // ---- home replies (batch_base relative to the home's first batch, indices batch-relative) ----
-    const uint32_t i = blockIdx.x * RT_T + threadIdx.x;
+    const uint32_t i = bid * RT_T + threadIdx.x;
     const bool home = i < w.E;
     const uint32_t code = home ? s.code[i] : (uint32_t)TB_CT_OK;
     const uint32_t bad = home && code != TB_CT_OK ? 1u : 0u;
     uint32_t tot;
-    const uint32_t rbad = seg_prefix<SEG>(s.cnt_bad, blockIdx.x, lds) + block_excl<SEG / 64>(bad, lds, &tot);
+    const uint32_t rbad = seg_prefix<SEG>(s.cnt_bad, bid, lds) + block_excl<SEG / 64>(bad, lds, &tot);
     if (home) {
       const uint32_t b = win_batch(w, i);
       if (i == w.off[b])
@@ -889,7 +945,7 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   }
   // the last block closes the window (the others read Globals::base, captured by k_rt_own, never the
   // counts written here)
-  if (blockIdx.x != gridDim.x - 1 || threadIdx.x != 0) return;
+  if (bid != nblk - 1 || threadIdx.x != 0) return;
   const uint64_t total = g->base + sh_total;
   g->events_total += w.E;
   g->windows_applied++;
