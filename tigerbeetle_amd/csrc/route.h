@@ -150,6 +150,7 @@ struct RtBufs {
   uint32_t claim_mask;
   unsigned long long* amt;  // owner: 64 slots x {low 32 bits, the rest} of the received amounts' sum
   uint32_t* hv;             // [0] the home verdict (k_rt_scan -> k_rt_decide)
+  u128* imax;               // owner: per k_rt_own id block, the largest received transfer id
 };
 
 __device__ inline uint32_t rt_lane_lt(unsigned long long m) {
@@ -530,6 +531,7 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
   const uint32_t k = b * RT_OWN_T + threadIdx.x;
   const bool live = k < sh_n;
   unsigned long long alo = 0, ahi = 0;
+  u128 idm = 0;
   if (!side) {
     if (live) {
       const uint8_t* rec = rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)k * 128;
@@ -538,6 +540,7 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
       // the id only (16 B): the rest of the record is read when a stored one must be compared
       const tb_uint128_t id = rw_u128(*reinterpret_cast<const uint4*>(rec));
       if (sh_claim) dup = rt_claim(rb.claim, rb.claim_mask, epoch, rt_id_base(L, sg) + k, id, rb.a_recv, L);
+      if (XFER) idm = U(id);
       if (XFER) {
         uint32_t xs = NONE32;
         if (x_may_exist(id, g->x_id_max)) {
@@ -551,6 +554,19 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
         code = slot == NONE32 ? (uint32_t)TB_CA_OK : ca_exists(*reinterpret_cast<const tb_account_t*>(rec), d.acc[slot]);
       }
       rb.b_send[rt_off_b(L, sg) + RT_HDR_B + k] = (uint8_t)((1u + code) | (dup ? RI_DUP : 0u));
+    }
+    if (XFER) {
+      // the block's largest received id, for the apply's bound on the stored ids (a bound over every
+      // received id holds over the committed ones; one plain store per block, no same-word atomics)
+      __shared__ u128 wmax[RT_OWN_T / 64];
+      idm = wave_max_u128(idm);
+      if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = idm;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        u128 mx = 0;
+        for (int w2 = 0; w2 < RT_OWN_T / 64; w2++) mx = umax128(mx, wmax[w2]);
+        rb.imax[blockIdx.x] = mx;
+      }
     }
   } else {
     if (live) {
@@ -634,11 +650,16 @@ __device__ inline uint32_t rt_code(const Scratch& s, const RtBufs& rb, const RtL
 template <bool XFER>
 __global__ void __launch_bounds__(RT_DEC_T) k_rt_decide(Dev d, Scratch s, RtBufs rb, WinDesc w, RtLayout L) {
   __shared__ uint32_t nbad, vsh;
+  __shared__ uint32_t cmin[RT_MAXG], ccnt[RT_MAXG][2];  // per destination: the block's first chunk, counts
   const uint32_t G = L.G, me = L.me;
   const uint64_t cb = rt_blk_c(L, me), ch = rt_c_hdr(L, me), cs = rt_c_side(L, me);
   if (threadIdx.x == 0) {
     nbad = 0;
     vsh = 0;
+  }
+  if (threadIdx.x < RT_MAXG) {
+    cmin[threadIdx.x] = NONE32;
+    ccnt[threadIdx.x][0] = ccnt[threadIdx.x][1] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     // the owners' verdicts (B headers, one lane each) and this home's (k_rt_scan), into every C header
@@ -699,21 +720,32 @@ __global__ void __launch_bounds__(RT_DEC_T) k_rt_decide(Dev d, Scratch s, RtBufs
       }
     }
   }
-  // committed id messages per (destination, chunk): one add per distinct key in the wave
+  // committed id messages per (destination, chunk), counted in LDS and added once per block: a block's
+  // messages to one destination are consecutive, so they span at most two chunks (one global add per
+  // wave and key had ~128 waves adding to each counter: same-address atomics serialize)
+  if (cdst != NONE32) atomicMin(&cmin[cdst], cchunk);
+  __syncthreads();
   const uint32_t key = cdst == NONE32 ? NONE32 : (cdst << 24) | cchunk;
   unsigned long long pend = __ballot(key != NONE32);
   while (pend) {
     const uint32_t leader = (uint32_t)__builtin_ctzll(pend);
     const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)leader);
     const unsigned long long m = __ballot(key == lk);
-    if ((threadIdx.x & 63) == leader)
-      atomicAdd(reinterpret_cast<uint32_t*>(rb.c_send + (lk >> 24) * cb + RT_HDR_C) + (lk & 0xFFFFFFu), (uint32_t)__popcll(m));
+    if ((threadIdx.x & 63) == leader) {
+      const uint32_t dd = lk >> 24, rel = (lk & 0xFFFFFFu) - cmin[dd];
+      if (rel < 2) atomicAdd(&ccnt[dd][rel], (uint32_t)__popcll(m));
+      else atomicAdd(reinterpret_cast<uint32_t*>(rb.c_send + dd * cb + RT_HDR_C) + (lk & 0xFFFFFFu), (uint32_t)__popcll(m));
+    }
     pend &= ~m;
   }
   const uint32_t wb = wave_sum(lbad);
   if ((threadIdx.x & 63) == 0 && wb) atomicAdd(&nbad, wb);
   if (verdict) atomicOr(&vsh, verdict);
   __syncthreads();
+  if (threadIdx.x < 2 * RT_MAXG) {
+    const uint32_t dd = threadIdx.x >> 1, rel = threadIdx.x & 1, c = ccnt[dd][rel];
+    if (c) atomicAdd(reinterpret_cast<uint32_t*>(rb.c_send + dd * cb + RT_HDR_C) + cmin[dd] + rel, c);
+  }
   if (threadIdx.x == 0 && nbad) atomicAdd(&s.cnt_bad[seg], nbad);
   if (vsh && threadIdx.x < G) atomicOr(reinterpret_cast<uint32_t*>(rb.c_send + threadIdx.x * cb), vsh);
 }
@@ -879,14 +911,15 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     // ---- account owner: the committed sides' balance adds ----
     const uint32_t k = sh_k0 + threadIdx.x;
     if (XFER && k < sh_n) {
-      const uint8_t* cc = rb.c_recv + rt_off_c(L, sg) + rt_c_side(L, sg);
-      if (cc[k]) {
-        uint32_t slot = rb.side_slot[rt_side_base(L, sg) + k];
-        const RtSide* m = reinterpret_cast<const RtSide*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A +
-                                                           (uint64_t)L.c1[sg] * 128 + (uint64_t)k * 32);
+      // the commit byte, the slot and the message's {amount, side} half loaded together (no chain)
+      const uint8_t commit = rb.c_recv[rt_off_c(L, sg) + rt_c_side(L, sg) + k];
+      const uint32_t slot = rb.side_slot[rt_side_base(L, sg) + k];
+      const uint4 m = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A +
+                                                     (uint64_t)L.c1[sg] * 128 + (uint64_t)k * 32)[1];
+      if (commit) {
         if (sh_guard(g, slot < d.acc_max, 3, slot)) {
-          const uint64_t amount = m->amount;
-          const uint32_t side = m->side;
+          const uint64_t amount = (uint64_t)m.x | ((uint64_t)m.y << 32);  // RtSide {id, amount, side, pad}
+          const uint32_t side = m.z;
           Add128 a;
           a.issue(side ? &d.acc[slot].credits_posted : &d.acc[slot].debits_posted, (u128)amount, sh_small != 0);
           if (chg.mark) chg.mark[slot] = chg_epoch;
@@ -904,33 +937,34 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     const uint32_t rank = sh_base + block_excl<RT_T / 64>(ins ? 1u : 0u, lds, &tot);
     const uint64_t slot = g->base + rank;
     const uint4* src = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)k * 128);
-    u128 idm = 0;
     if (XFER) {
       const bool prefix_win = (g->win_flags & 2u) != 0;
-      if (ins && sh_guard(g, slot < d.x_max, 5, slot)) {
+      const unsigned long long ml = __ballot(live), mi = __ballot(ins);
+      const uint32_t n = (uint32_t)__popcll(ml), lane = threadIdx.x & 63;
+      const uint64_t slot0 = g->base + (uint32_t)__builtin_amdgcn_readlane((int)rank, 0);
+      if (prefix_win && mi == ml && slot0 + n <= d.x_max) {
+        // every live message of this wave commits and the window appends above every stored id (no
+        // table insert): the wave's records are one run in the A buffer and one in the store, copied
+        // as 16 B words lane by lane, so each load / store instruction covers one contiguous KiB (a
+        // record per lane put 64 lines into every instruction, and every store was a partial line)
+        const uint4* src0 = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)(k - lane) * 128);
+        uint4* dst0 = reinterpret_cast<uint4*>(d.xr + slot0);
+        uint4 v[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) v[j] = lane + 64 * j < n * 8 ? src0[lane + 64 * j] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+          if (lane + 64 * j < n * 8) st_stream(dst0 + lane + 64 * j, v[j]);
+        if (ins) d.xstatus[slot] = 0;
+      } else if (ins && sh_guard(g, slot < d.x_max, 5, slot)) {
         uint4 r[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) r[q] = src[q];
         uint4* dst = reinterpret_cast<uint4*>(d.xr + slot);
 #pragma unroll
         for (int q = 0; q < 8; q++) st_stream(dst + q, r[q]);
-        const tb_uint128_t id = rw_u128(r[0]);
-        idm = U(id);
-        if (!prefix_win) x_insert(d.x_tab, d.x_mask, id, (uint32_t)slot);
+        if (!prefix_win) x_insert(d.x_tab, d.x_mask, rw_u128(r[0]), (uint32_t)slot);
         d.xstatus[slot] = 0;
-      }
-      idm = wave_max_u128(idm);
-      if ((threadIdx.x & 63) == 0) sh_imax[threadIdx.x >> 6] = idm;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        u128 mx = 0;
-        for (int w2 = 0; w2 < RT_T / 64; w2++) mx = umax128(mx, sh_imax[w2]);
-        // a word-wise upper bound on the stored ids (can only disable a prefix extension)
-        if (mx > g->x_id_max) {
-          unsigned long long* xm = reinterpret_cast<unsigned long long*>(&g->x_id_max);
-          atomicMax(xm + 1, (unsigned long long)(mx >> 64));
-          atomicMax(xm, (unsigned long long)mx);
-        }
       }
     } else if (ins && sh_guard(g, slot < d.acc_max, 6, slot)) {
       uint4 r[8];
@@ -945,7 +979,22 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   }
   // the last block closes the window (the others read Globals::base, captured by k_rt_own, never the
   // counts written here)
-  if (bid != nblk - 1 || threadIdx.x != 0) return;
+  if (bid != nblk - 1) return;
+  u128 mx = 0;
+  if (XFER) {
+    // the bound on the stored ids: the largest id k_rt_own's blocks received (an upper bound: it can
+    // only disable a prefix extension), folded by this block
+    uint32_t id_blocks = 0;
+    (void)rt_own_blocks(L, &id_blocks);
+    for (uint32_t q = threadIdx.x; q < id_blocks; q += RT_T) mx = umax128(mx, rb.imax[q]);
+    mx = wave_max_u128(mx);
+    if ((threadIdx.x & 63) == 0) sh_imax[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int w2 = 0; w2 < RT_T / 64; w2++) mx = umax128(mx, sh_imax[w2]);
+  }
+  if (threadIdx.x != 0) return;
+  if (XFER && mx > g->x_id_max) g->x_id_max = mx;
   const uint64_t total = g->base + sh_total;
   g->events_total += w.E;
   g->windows_applied++;
