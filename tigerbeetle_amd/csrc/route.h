@@ -772,55 +772,51 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   // (b_off / nblk: the grid may be launched in parts, one per role — TBG_RT_SPLIT, a profiling aid)
   const uint32_t bid = blockIdx.x + b_off;
   __shared__ uint32_t lds[RT_T / 64];
-  __shared__ uint32_t sh_v, sh_src, sh_k0, sh_n, sh_role, sh_base, sh_total;
-  __shared__ unsigned long long sh_small;
+  __shared__ uint32_t f_v, sh_base, sh_total;
+  __shared__ unsigned long long f_amt[2];
+  __shared__ uint32_t f_cnt[RT_T / 64][2];
   __shared__ u128 sh_imax[RT_T / 64];
   Globals* g = d.g;
   const uint32_t G = L.G;
-  if (threadIdx.x == 0) {
-    uint32_t b = bid, role = 0, sg = 0, k0 = 0;
-    if (b >= nh) {
-      b -= nh;
-      role = 1;
+  // this block's role, source shard and first message (kernel arguments only: the same in every thread)
+  uint32_t b = bid, role = 0, sg = 0, k0 = 0, my_flat = 0;
+  if (b >= nh) {
+    b -= nh;
+    role = 1;
+    for (sg = 0; sg < G; sg++) {
+      const uint32_t nb = (L.c2[sg] + RT_T - 1) / RT_T;
+      if (b < nb) break;
+      b -= nb;
+    }
+    k0 = b * RT_T;
+    if (sg == G) {
+      role = 2;
+      my_flat = b;  // (the id blocks are the chunks in (source, chunk) order: this one's flat index)
       for (sg = 0; sg < G; sg++) {
-        const uint32_t nb = (L.c2[sg] + RT_T - 1) / RT_T;
+        const uint32_t nb = rt_nch(L.c1[sg]);
         if (b < nb) break;
         b -= nb;
       }
-      k0 = b * RT_T;
-      if (sg == G) {
-        role = 2;
-        sh_base = b;  // (the id blocks are the chunks in (source, chunk) order: this one's flat index)
-        for (sg = 0; sg < G; sg++) {
-          const uint32_t nb = rt_nch(L.c1[sg]);
-          if (b < nb) break;
-          b -= nb;
-        }
-        k0 = b * RT_CHUNK;
-      }
+      k0 = b * RT_CHUNK;
     }
-    sh_role = role;
-    sh_src = sg;
-    sh_k0 = k0;
-    const RtHdrA* h = sg < G ? reinterpret_cast<const RtHdrA*>(rb.a_recv + rt_off_a(L, sg)) : nullptr;
-    sh_n = h ? (role == 1 ? h->n_side : h->n_id) : 0u;
   }
-  // what every block folds from the G C headers, in parallel: the verdict; the committed records in all
-  // and, for an id block, before its chunk ((source, chunk) order); for a side block, whether the
-  // received amounts keep every balance field below 2^64
-  __shared__ uint32_t f_v;
-  __shared__ unsigned long long f_amt[2];
+  const bool last = bid == nblk - 1;
+  const RtHdrA* hdr = role && sg < G ? reinterpret_cast<const RtHdrA*>(rb.a_recv + rt_off_a(L, sg)) : nullptr;
+  const uint32_t n_msg = hdr ? (role == 1 ? hdr->n_side : hdr->n_id) : 0u;
+  // what a block folds from the G C headers, in parallel: the verdict (every block); the committed
+  // records before its chunk ((source, chunk) order: id blocks) and in all (the last block); whether
+  // the received amounts keep every balance field below 2^64 (side blocks)
   if (threadIdx.x == 0) {
     f_v = 0;
     f_amt[0] = f_amt[1] = 0;
   }
   __syncthreads();
   if (threadIdx.x < G) atomicOr(&f_v, *reinterpret_cast<const uint32_t*>(rb.c_recv + rt_off_c(L, threadIdx.x)));
-  const uint32_t my_flat = sh_role == 2 ? sh_base : 0u;
-  uint32_t before = 0, all = 0;
-  {
+  const bool counts = role == 2 || last;
+  if (counts) {
     // one count per thread and source (a source has at most RT_T chunks unless its capacity passes 1M
     // messages: the loop after takes the rest); the G loads are issued before any is used
+    uint32_t before = 0, all = 0;
     uint32_t v[RT_MAXG], fl[RT_MAXG];
     uint32_t flat0 = 0;
     uint64_t off = 0;
@@ -852,8 +848,14 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
         flat0 += nch;
       }
     }
+    before = wave_sum(before);
+    all = wave_sum(all);
+    if ((threadIdx.x & 63) == 0) {
+      f_cnt[threadIdx.x >> 6][0] = before;
+      f_cnt[threadIdx.x >> 6][1] = all;
+    }
   }
-  if (XFER && sh_role == 1 && threadIdx.x < 64) {
+  if (XFER && role == 1 && threadIdx.x < 64) {
     unsigned long long lo = rb.amt[threadIdx.x * 2], hi = rb.amt[threadIdx.x * 2 + 1];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -865,24 +867,27 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
       f_amt[1] = hi;
     }
   }
-  all = block_sum<RT_T / 64>(all, lds);
-  before = block_sum<RT_T / 64>(before, lds);
-  if (threadIdx.x == 0) {
-    sh_v = f_v;
-    sh_total = all;
-    if (sh_role == 2) sh_base = before;
-    if (XFER && sh_role == 1) {
-      const u128 tot = (u128)f_amt[0] + ((u128)f_amt[1] << 32);
-      const u128 top = g->ovf_bound + tot;
-      sh_small = (top >= g->ovf_bound && (uint64_t)(top >> 64) == 0) ? 1ull : 0ull;
-    }
-  }
   __syncthreads();
-  if (sh_v) {
-    if (bid == nblk - 1 && threadIdx.x == 0) atomicOr(&g->window_error, 2u);
+  if (counts && threadIdx.x == 0) {
+    uint32_t before = 0, all = 0;
+    for (int w2 = 0; w2 < RT_T / 64; w2++) {
+      before += f_cnt[w2][0];
+      all += f_cnt[w2][1];
+    }
+    sh_base = before;
+    sh_total = all;
+  }
+  bool small = false;
+  if (XFER && role == 1) {
+    const u128 tot = (u128)f_amt[0] + ((u128)f_amt[1] << 32);
+    const u128 top = g->ovf_bound + tot;
+    small = top >= g->ovf_bound && (uint64_t)(top >> 64) == 0;
+  }
+  if (counts) __syncthreads();
+  if (f_v) {
+    if (last && threadIdx.x == 0) atomicOr(&g->window_error, 2u);
     return;
   }
-  const uint32_t role = sh_role, sg = sh_src;
   if (role == 0) {
     // ---- home replies (batch_base relative to the home's first batch, indices batch-relative) ----
     const uint32_t i = bid * RT_T + threadIdx.x;
@@ -909,8 +914,8 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     }
   } else if (role == 1) {
     // ---- account owner: the committed sides' balance adds ----
-    const uint32_t k = sh_k0 + threadIdx.x;
-    if (XFER && k < sh_n) {
+    const uint32_t k = k0 + threadIdx.x;
+    if (XFER && k < n_msg) {
       // the commit byte, the slot and the message's {amount, side} half loaded together (no chain)
       const uint8_t commit = rb.c_recv[rt_off_c(L, sg) + rt_c_side(L, sg) + k];
       const uint32_t slot = rb.side_slot[rt_side_base(L, sg) + k];
@@ -921,7 +926,7 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
           const uint64_t amount = (uint64_t)m.x | ((uint64_t)m.y << 32);  // RtSide {id, amount, side, pad}
           const uint32_t side = m.z;
           Add128 a;
-          a.issue(side ? &d.acc[slot].credits_posted : &d.acc[slot].debits_posted, (u128)amount, sh_small != 0);
+          a.issue(side ? &d.acc[slot].credits_posted : &d.acc[slot].debits_posted, (u128)amount, small);
           if (chg.mark) chg.mark[slot] = chg_epoch;
           a.finish();
         }
@@ -929,8 +934,8 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     }
   } else {
     // ---- id owner: committed records appended at base + rank, (source, message) order ----
-    const uint32_t k = sh_k0 + threadIdx.x;
-    const bool live = k < sh_n;
+    const uint32_t k = k0 + threadIdx.x;
+    const bool live = k < n_msg;
     const uint8_t* cc = rb.c_recv + rt_off_c(L, sg) + rt_c_hdr(L, sg);
     const bool ins = live && cc[k] != 0;
     uint32_t tot;
