@@ -469,18 +469,37 @@ __device__ inline RtAFold rt_fold_a(const uint8_t* a_recv, const RtLayout& L, ui
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_rt_own (owner, after exchange A): one received message per thread. Blocks: for each source shard
-// its id messages (ceil(c1 / 256) blocks), then for each its side messages.
+// k_rt_own (owner, after exchange A): RT_OWN_J received messages per thread (their loads, and the
+// first table probe of every side, issued together: the kernel is a chain of dependent random reads,
+// so it is paced by how many are in flight). Blocks: for each source shard its id messages
+// (ceil(c1 / RT_OWN_M) blocks), then for each its side messages.
 // ------------------------------------------------------------------------------------------------
 #define RT_OWN_T 256
+#define RT_OWN_J 4
+#define RT_OWN_M (RT_OWN_T * RT_OWN_J)
 __host__ __device__ inline uint32_t rt_own_blocks(const RtLayout& L, uint32_t* id_blocks) {
   uint32_t a = 0, b = 0;
   for (uint32_t sg = 0; sg < L.G; sg++) {
-    a += (L.c1[sg] + RT_OWN_T - 1) / RT_OWN_T;
-    b += (L.c2[sg] + RT_OWN_T - 1) / RT_OWN_T;
+    a += (L.c1[sg] + RT_OWN_M - 1) / RT_OWN_M;
+    b += (L.c2[sg] + RT_OWN_M - 1) / RT_OWN_M;
   }
   if (id_blocks) *id_blocks = a;
   return a + b;
+}
+
+// acc_find (dev_common.h) continued from its first entry `e` at `h`, already loaded
+__device__ inline uint32_t rt_acc_probe_from(const AccEntry* __restrict__ tab, uint64_t mask, tb_uint128_t id, uint64_t h,
+                                             AccEntry e, AccEntry* out) {
+  if ((id.lo | id.hi) == 0) return NONE32;
+  for (;;) {
+    if (e.slot == NONE32) return NONE32;
+    if (e.id_lo == id.lo && e.id_hi == id.hi) {
+      *out = e;
+      return e.slot;
+    }
+    h = (h + 1) & mask;
+    e = tab[h];
+  }
 }
 
 template <bool XFER>
@@ -492,14 +511,14 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
   // this block's source shard and first message (kernel arguments only: the same in every thread)
   uint32_t b = blockIdx.x, side = 0, sg = 0;
   for (; sg < G; sg++) {
-    const uint32_t nb = (L.c1[sg] + RT_OWN_T - 1) / RT_OWN_T;
+    const uint32_t nb = (L.c1[sg] + RT_OWN_M - 1) / RT_OWN_M;
     if (b < nb) break;
     b -= nb;
   }
   if (sg == G) {
     side = 1;
     for (sg = 0; sg < G; sg++) {
-      const uint32_t nb = (L.c2[sg] + RT_OWN_T - 1) / RT_OWN_T;
+      const uint32_t nb = (L.c2[sg] + RT_OWN_M - 1) / RT_OWN_M;
       if (b < nb) break;
       b -= nb;
     }
@@ -528,20 +547,30 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
   }
   __syncthreads();
   if (sg >= G) return;
-  const uint32_t k = b * RT_OWN_T + threadIdx.x;
-  const bool live = k < sh_n;
-  unsigned long long alo = 0, ahi = 0;
-  u128 idm = 0;
+  const uint32_t k0 = b * RT_OWN_M + threadIdx.x, n = sh_n;
   if (!side) {
-    if (live) {
-      const uint8_t* rec = rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)k * 128;
+    // ---- id messages: claim (ids not known to rise), exists against a stored record ----
+    const uint8_t* base = rb.a_recv + rt_off_a(L, sg) + RT_HDR_A;
+    tb_uint128_t ids[RT_OWN_J];
+#pragma unroll
+    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+      // the id only (16 B): the rest of the record is read when a stored one must be compared
+      const uint32_t k = k0 + j * RT_OWN_T;
+      ids[j] = k < n ? rw_u128(*reinterpret_cast<const uint4*>(base + (uint64_t)k * 128)) : tb_uint128_t{0, 0};
+    }
+    u128 idm = 0;
+    const bool claim = sh_claim != 0;
+#pragma unroll
+    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+      const uint32_t k = k0 + j * RT_OWN_T;
+      if (k >= n) continue;
+      const tb_uint128_t id = ids[j];
+      const uint8_t* rec = base + (uint64_t)k * 128;
       uint32_t code;
       bool dup = false;
-      // the id only (16 B): the rest of the record is read when a stored one must be compared
-      const tb_uint128_t id = rw_u128(*reinterpret_cast<const uint4*>(rec));
-      if (sh_claim) dup = rt_claim(rb.claim, rb.claim_mask, epoch, rt_id_base(L, sg) + k, id, rb.a_recv, L);
-      if (XFER) idm = U(id);
+      if (claim) dup = rt_claim(rb.claim, rb.claim_mask, epoch, rt_id_base(L, sg) + k, id, rb.a_recv, L);
       if (XFER) {
+        idm = umax128(idm, U(id));
         uint32_t xs = NONE32;
         if (x_may_exist(id, g->x_id_max)) {
           xs = x_find(d.x_tab, d.xr, d.x_mask, id);
@@ -569,25 +598,42 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
       }
     }
   } else {
-    if (live) {
-      const RtSide m = *reinterpret_cast<const RtSide*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A +
-                                                         (uint64_t)L.c1[sg] * 128 + (uint64_t)k * 32);
-      tb_uint128_t id;
-      id.lo = m.id_lo;
-      id.hi = m.id_hi;
+    // ---- side messages: the account's slot (kept for the apply), ledger and limit / history flag ----
+    const uint8_t* base = rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)L.c1[sg] * 128;
+    uint4 mid[RT_OWN_J], mam[RT_OWN_J];  // RtSide {id}, {amount, side, pad}
+#pragma unroll
+    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+      const uint32_t k = k0 + j * RT_OWN_T;
+      const uint4* m = reinterpret_cast<const uint4*>(base + (uint64_t)k * 32);
+      mid[j] = k < n ? m[0] : make_uint4(0, 0, 0, 0);
+      mam[j] = k < n ? m[1] : make_uint4(0, 0, 0, 0);
+    }
+    uint64_t hh[RT_OWN_J];
+    AccEntry e0[RT_OWN_J];
+#pragma unroll
+    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+      const tb_uint128_t id = rw_u128(mid[j]);
+      hh[j] = hash_id(id.lo, id.hi) & d.acc_mask;
+      if (k0 + j * RT_OWN_T < n) e0[j] = d.acc_tab[hh[j]];
+    }
+    unsigned long long alo = 0, ahi = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+      const uint32_t k = k0 + j * RT_OWN_T;
+      if (k >= n) continue;
       AccEntry e;
-      const uint32_t slot = acc_find(d.acc_tab, d.acc_mask, id, &e);
+      const uint32_t slot = rt_acc_probe_from(d.acc_tab, d.acc_mask, rw_u128(mid[j]), hh[j], e0[j], &e);
       rb.side_slot[rt_side_base(L, sg) + k] = slot;
       uint32_t st = 0, ledger = 0;
       if (slot != NONE32) {
         st = RS_FOUND;
         ledger = e.ledger;
-        const uint16_t lim = m.side ? TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS : TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS;
+        const uint16_t lim = mam[j].z ? TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS : TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS;
         if (e.flags & (lim | TB_ACCOUNT_HISTORY)) st |= RS_LIMIT;
       }
       *reinterpret_cast<uint2*>(rb.b_send + rt_off_b(L, sg) + rt_b_side(L, sg) + (uint64_t)k * 8) = make_uint2(ledger, st);
-      alo = m.amount & 0xFFFFFFFFull;
-      ahi = m.amount >> 32;
+      alo += mam[j].x;  // the amount's low and high 32 bits
+      ahi += mam[j].y;
     }
     // the received amounts' sum (a bound on this window's balance growth here): 64 slots, no-return adds
 #pragma unroll
