@@ -83,7 +83,7 @@ enum : uint32_t { RI_CODE = 0x3F, RI_DUP = 0x40 };
 struct RtLayout {
   uint32_t G, me;
   uint32_t xfer;
-  uint32_t pad;
+  uint32_t own_j;        // received messages per k_rt_own thread (1 or RT_OWN_J; local to the shard)
   uint32_t n[RT_MAXG];   // home events
   uint32_t c1[RT_MAXG];  // id messages per destination block (capacity)
   uint32_t c2[RT_MAXG];  // side messages per destination block
@@ -469,19 +469,19 @@ __device__ inline RtAFold rt_fold_a(const uint8_t* a_recv, const RtLayout& L, ui
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_rt_own (owner, after exchange A): RT_OWN_J received messages per thread (their loads, and the
+// k_rt_own (owner, after exchange A): J received messages per thread (their loads, and the
 // first table probe of every side, issued together: the kernel is a chain of dependent random reads,
 // so it is paced by how many are in flight). Blocks: for each source shard its id messages
-// (ceil(c1 / RT_OWN_M) blocks), then for each its side messages.
+// (ceil(c1 / (256 J)) blocks), then for each its side messages.
 // ------------------------------------------------------------------------------------------------
 #define RT_OWN_T 256
-#define RT_OWN_J 4
-#define RT_OWN_M (RT_OWN_T * RT_OWN_J)
+#define RT_OWN_J 4  // (four per thread when one per thread would take more than two rounds of resident blocks)
 __host__ __device__ inline uint32_t rt_own_blocks(const RtLayout& L, uint32_t* id_blocks) {
+  const uint32_t M = RT_OWN_T * (L.own_j ? L.own_j : 1u);
   uint32_t a = 0, b = 0;
   for (uint32_t sg = 0; sg < L.G; sg++) {
-    a += (L.c1[sg] + RT_OWN_M - 1) / RT_OWN_M;
-    b += (L.c2[sg] + RT_OWN_M - 1) / RT_OWN_M;
+    a += (L.c1[sg] + M - 1) / M;
+    b += (L.c2[sg] + M - 1) / M;
   }
   if (id_blocks) *id_blocks = a;
   return a + b;
@@ -502,7 +502,7 @@ __device__ inline uint32_t rt_acc_probe_from(const AccEntry* __restrict__ tab, u
   }
 }
 
-template <bool XFER>
+template <bool XFER, uint32_t J>
 __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout L, uint32_t epoch) {
   __shared__ uint32_t sh_n, sh_claim;
   __shared__ unsigned long long ared[RT_OWN_T / 64][2];
@@ -511,14 +511,14 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
   // this block's source shard and first message (kernel arguments only: the same in every thread)
   uint32_t b = blockIdx.x, side = 0, sg = 0;
   for (; sg < G; sg++) {
-    const uint32_t nb = (L.c1[sg] + RT_OWN_M - 1) / RT_OWN_M;
+    const uint32_t nb = (L.c1[sg] + (RT_OWN_T * J) - 1) / (RT_OWN_T * J);
     if (b < nb) break;
     b -= nb;
   }
   if (sg == G) {
     side = 1;
     for (sg = 0; sg < G; sg++) {
-      const uint32_t nb = (L.c2[sg] + RT_OWN_M - 1) / RT_OWN_M;
+      const uint32_t nb = (L.c2[sg] + (RT_OWN_T * J) - 1) / (RT_OWN_T * J);
       if (b < nb) break;
       b -= nb;
     }
@@ -547,13 +547,13 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
   }
   __syncthreads();
   if (sg >= G) return;
-  const uint32_t k0 = b * RT_OWN_M + threadIdx.x, n = sh_n;
+  const uint32_t k0 = b * (RT_OWN_T * J) + threadIdx.x, n = sh_n;
   if (!side) {
     // ---- id messages: claim (ids not known to rise), exists against a stored record ----
     const uint8_t* base = rb.a_recv + rt_off_a(L, sg) + RT_HDR_A;
-    tb_uint128_t ids[RT_OWN_J];
+    tb_uint128_t ids[J];
 #pragma unroll
-    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+    for (uint32_t j = 0; j < J; j++) {
       // the id only (16 B): the rest of the record is read when a stored one must be compared
       const uint32_t k = k0 + j * RT_OWN_T;
       ids[j] = k < n ? rw_u128(*reinterpret_cast<const uint4*>(base + (uint64_t)k * 128)) : tb_uint128_t{0, 0};
@@ -561,7 +561,7 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
     u128 idm = 0;
     const bool claim = sh_claim != 0;
 #pragma unroll
-    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+    for (uint32_t j = 0; j < J; j++) {
       const uint32_t k = k0 + j * RT_OWN_T;
       if (k >= n) continue;
       const tb_uint128_t id = ids[j];
@@ -600,25 +600,25 @@ __global__ void __launch_bounds__(RT_OWN_T) k_rt_own(Dev d, RtBufs rb, RtLayout 
   } else {
     // ---- side messages: the account's slot (kept for the apply), ledger and limit / history flag ----
     const uint8_t* base = rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)L.c1[sg] * 128;
-    uint4 mid[RT_OWN_J], mam[RT_OWN_J];  // RtSide {id}, {amount, side, pad}
+    uint4 mid[J], mam[J];  // RtSide {id}, {amount, side, pad}
 #pragma unroll
-    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+    for (uint32_t j = 0; j < J; j++) {
       const uint32_t k = k0 + j * RT_OWN_T;
       const uint4* m = reinterpret_cast<const uint4*>(base + (uint64_t)k * 32);
       mid[j] = k < n ? m[0] : make_uint4(0, 0, 0, 0);
       mam[j] = k < n ? m[1] : make_uint4(0, 0, 0, 0);
     }
-    uint64_t hh[RT_OWN_J];
-    AccEntry e0[RT_OWN_J];
+    uint64_t hh[J];
+    AccEntry e0[J];
 #pragma unroll
-    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+    for (uint32_t j = 0; j < J; j++) {
       const tb_uint128_t id = rw_u128(mid[j]);
       hh[j] = hash_id(id.lo, id.hi) & d.acc_mask;
       if (k0 + j * RT_OWN_T < n) e0[j] = d.acc_tab[hh[j]];
     }
     unsigned long long alo = 0, ahi = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < RT_OWN_J; j++) {
+    for (uint32_t j = 0; j < J; j++) {
       const uint32_t k = k0 + j * RT_OWN_T;
       if (k >= n) continue;
       AccEntry e;
@@ -849,6 +849,33 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   const bool last = bid == nblk - 1;
   const RtHdrA* hdr = role && sg < G ? reinterpret_cast<const RtHdrA*>(rb.a_recv + rt_off_a(L, sg)) : nullptr;
   const uint32_t n_msg = hdr ? (role == 1 ? hdr->n_side : hdr->n_id) : 0u;
+  // the role's own inputs, issued before the folds below and bounded by the block's capacity, not by
+  // n_msg (independent of both, so their latency overlaps the folds'; what lies past n_msg is never used)
+  const uint32_t kk = k0 + threadIdx.x, lane = threadIdx.x & 63;
+  uint32_t in_code = TB_CT_OK;                // home: the event's code
+  uint8_t in_commit = 0;                      // side / id: the message's commit byte
+  uint32_t in_slot = NONE32;                  // side: the account slot
+  uint4 in_m = make_uint4(0, 0, 0, 0);        // side: RtSide's {amount, side, pad} half
+  uint4 in_v[8];                              // id (transfers): the wave's records as lane-contiguous words
+  if (role == 0) {
+    if (bid * RT_T + threadIdx.x < w.E) in_code = s.code[bid * RT_T + threadIdx.x];
+  } else if (role == 1) {
+    if (XFER && sg < G && kk < L.c2[sg]) {
+      in_commit = rb.c_recv[rt_off_c(L, sg) + rt_c_side(L, sg) + kk];
+      in_slot = rb.side_slot[rt_side_base(L, sg) + kk];
+      in_m = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)L.c1[sg] * 128 +
+                                            (uint64_t)kk * 32)[1];
+    }
+  } else if (sg < G) {
+    if (kk < L.c1[sg]) in_commit = rb.c_recv[rt_off_c(L, sg) + rt_c_hdr(L, sg) + kk];
+    if (XFER) {
+      const uint32_t kw = kk - lane;  // the wave's first message
+      const uint4* src0 = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)kw * 128);
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++)
+        in_v[j] = kw + (lane + 64 * j) / 8 < L.c1[sg] ? src0[lane + 64 * j] : make_uint4(0, 0, 0, 0);
+    }
+  }
   // what a block folds from the G C headers, in parallel: the verdict (every block); the committed
   // records before its chunk ((source, chunk) order: id blocks) and in all (the last block); whether
   // the received amounts keep every balance field below 2^64 (side blocks)
@@ -938,7 +965,7 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     // ---- home replies (batch_base relative to the home's first batch, indices batch-relative) ----
     const uint32_t i = bid * RT_T + threadIdx.x;
     const bool home = i < w.E;
-    const uint32_t code = home ? s.code[i] : (uint32_t)TB_CT_OK;
+    const uint32_t code = in_code;
     const uint32_t bad = home && code != TB_CT_OK ? 1u : 0u;
     uint32_t tot;
     const uint32_t rbad = seg_prefix<SEG>(s.cnt_bad, bid, lds) + block_excl<SEG / 64>(bad, lds, &tot);
@@ -960,14 +987,10 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     }
   } else if (role == 1) {
     // ---- account owner: the committed sides' balance adds ----
-    const uint32_t k = k0 + threadIdx.x;
-    if (XFER && k < n_msg) {
-      // the commit byte, the slot and the message's {amount, side} half loaded together (no chain)
-      const uint8_t commit = rb.c_recv[rt_off_c(L, sg) + rt_c_side(L, sg) + k];
-      const uint32_t slot = rb.side_slot[rt_side_base(L, sg) + k];
-      const uint4 m = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A +
-                                                     (uint64_t)L.c1[sg] * 128 + (uint64_t)k * 32)[1];
-      if (commit) {
+    if (XFER && kk < n_msg) {
+      const uint32_t slot = in_slot;
+      const uint4 m = in_m;
+      if (in_commit) {
         if (sh_guard(g, slot < d.acc_max, 3, slot)) {
           const uint64_t amount = (uint64_t)m.x | ((uint64_t)m.y << 32);  // RtSide {id, amount, side, pad}
           const uint32_t side = m.z;
@@ -980,10 +1003,9 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     }
   } else {
     // ---- id owner: committed records appended at base + rank, (source, message) order ----
-    const uint32_t k = k0 + threadIdx.x;
+    const uint32_t k = kk;
     const bool live = k < n_msg;
-    const uint8_t* cc = rb.c_recv + rt_off_c(L, sg) + rt_c_hdr(L, sg);
-    const bool ins = live && cc[k] != 0;
+    const bool ins = live && in_commit != 0;
     uint32_t tot;
     const uint32_t rank = sh_base + block_excl<RT_T / 64>(ins ? 1u : 0u, lds, &tot);
     const uint64_t slot = g->base + rank;
@@ -991,21 +1013,17 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     if (XFER) {
       const bool prefix_win = (g->win_flags & 2u) != 0;
       const unsigned long long ml = __ballot(live), mi = __ballot(ins);
-      const uint32_t n = (uint32_t)__popcll(ml), lane = threadIdx.x & 63;
+      const uint32_t n = (uint32_t)__popcll(ml);
       const uint64_t slot0 = g->base + (uint32_t)__builtin_amdgcn_readlane((int)rank, 0);
       if (prefix_win && mi == ml && slot0 + n <= d.x_max) {
         // every live message of this wave commits and the window appends above every stored id (no
         // table insert): the wave's records are one run in the A buffer and one in the store, copied
-        // as 16 B words lane by lane, so each load / store instruction covers one contiguous KiB (a
-        // record per lane put 64 lines into every instruction, and every store was a partial line)
-        const uint4* src0 = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)(k - lane) * 128);
+        // as 16 B words lane by lane (loaded above), so each load / store instruction covers one
+        // contiguous KiB (a record per lane put 64 lines into every instruction, every store a partial line)
         uint4* dst0 = reinterpret_cast<uint4*>(d.xr + slot0);
-        uint4 v[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) v[j] = lane + 64 * j < n * 8 ? src0[lane + 64 * j] : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++)
-          if (lane + 64 * j < n * 8) st_stream(dst0 + lane + 64 * j, v[j]);
+          if (lane + 64 * j < n * 8) st_stream(dst0 + lane + 64 * j, in_v[j]);
         if (ins) d.xstatus[slot] = 0;
       } else if (ins && sh_guard(g, slot < d.x_max, 5, slot)) {
         uint4 r[8];
