@@ -849,33 +849,6 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
   const bool last = bid == nblk - 1;
   const RtHdrA* hdr = role && sg < G ? reinterpret_cast<const RtHdrA*>(rb.a_recv + rt_off_a(L, sg)) : nullptr;
   const uint32_t n_msg = hdr ? (role == 1 ? hdr->n_side : hdr->n_id) : 0u;
-  // the role's own inputs, issued before the folds below and bounded by the block's capacity, not by
-  // n_msg (independent of both, so their latency overlaps the folds'; what lies past n_msg is never used)
-  const uint32_t kk = k0 + threadIdx.x, lane = threadIdx.x & 63;
-  uint32_t in_code = TB_CT_OK;                // home: the event's code
-  uint8_t in_commit = 0;                      // side / id: the message's commit byte
-  uint32_t in_slot = NONE32;                  // side: the account slot
-  uint4 in_m = make_uint4(0, 0, 0, 0);        // side: RtSide's {amount, side, pad} half
-  uint4 in_v[8];                              // id (transfers): the wave's records as lane-contiguous words
-  if (role == 0) {
-    if (bid * RT_T + threadIdx.x < w.E) in_code = s.code[bid * RT_T + threadIdx.x];
-  } else if (role == 1) {
-    if (XFER && sg < G && kk < L.c2[sg]) {
-      in_commit = rb.c_recv[rt_off_c(L, sg) + rt_c_side(L, sg) + kk];
-      in_slot = rb.side_slot[rt_side_base(L, sg) + kk];
-      in_m = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)L.c1[sg] * 128 +
-                                            (uint64_t)kk * 32)[1];
-    }
-  } else if (sg < G) {
-    if (kk < L.c1[sg]) in_commit = rb.c_recv[rt_off_c(L, sg) + rt_c_hdr(L, sg) + kk];
-    if (XFER) {
-      const uint32_t kw = kk - lane;  // the wave's first message
-      const uint4* src0 = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)kw * 128);
-#pragma unroll
-      for (uint32_t j = 0; j < 8; j++)
-        in_v[j] = kw + (lane + 64 * j) / 8 < L.c1[sg] ? src0[lane + 64 * j] : make_uint4(0, 0, 0, 0);
-    }
-  }
   // what a block folds from the G C headers, in parallel: the verdict (every block); the committed
   // records before its chunk ((source, chunk) order: id blocks) and in all (the last block); whether
   // the received amounts keep every balance field below 2^64 (side blocks)
@@ -965,7 +938,7 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     // ---- home replies (batch_base relative to the home's first batch, indices batch-relative) ----
     const uint32_t i = bid * RT_T + threadIdx.x;
     const bool home = i < w.E;
-    const uint32_t code = in_code;
+    const uint32_t code = home ? s.code[i] : (uint32_t)TB_CT_OK;
     const uint32_t bad = home && code != TB_CT_OK ? 1u : 0u;
     uint32_t tot;
     const uint32_t rbad = seg_prefix<SEG>(s.cnt_bad, bid, lds) + block_excl<SEG / 64>(bad, lds, &tot);
@@ -987,10 +960,14 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     }
   } else if (role == 1) {
     // ---- account owner: the committed sides' balance adds ----
-    if (XFER && kk < n_msg) {
-      const uint32_t slot = in_slot;
-      const uint4 m = in_m;
-      if (in_commit) {
+    const uint32_t k = k0 + threadIdx.x;
+    if (XFER && k < n_msg) {
+      // the commit byte, the slot and the message's {amount, side} half loaded together (no chain)
+      const uint8_t commit = rb.c_recv[rt_off_c(L, sg) + rt_c_side(L, sg) + k];
+      const uint32_t slot = rb.side_slot[rt_side_base(L, sg) + k];
+      const uint4 m = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A +
+                                                     (uint64_t)L.c1[sg] * 128 + (uint64_t)k * 32)[1];
+      if (commit) {
         if (sh_guard(g, slot < d.acc_max, 3, slot)) {
           const uint64_t amount = (uint64_t)m.x | ((uint64_t)m.y << 32);  // RtSide {id, amount, side, pad}
           const uint32_t side = m.z;
@@ -1003,9 +980,10 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     }
   } else {
     // ---- id owner: committed records appended at base + rank, (source, message) order ----
-    const uint32_t k = kk;
+    const uint32_t k = k0 + threadIdx.x;
     const bool live = k < n_msg;
-    const bool ins = live && in_commit != 0;
+    const uint8_t* cc = rb.c_recv + rt_off_c(L, sg) + rt_c_hdr(L, sg);
+    const bool ins = live && cc[k] != 0;
     uint32_t tot;
     const uint32_t rank = sh_base + block_excl<RT_T / 64>(ins ? 1u : 0u, lds, &tot);
     const uint64_t slot = g->base + rank;
@@ -1013,17 +991,21 @@ __global__ void __launch_bounds__(RT_T) k_rt_apply(Dev d, Scratch s, RtBufs rb, 
     if (XFER) {
       const bool prefix_win = (g->win_flags & 2u) != 0;
       const unsigned long long ml = __ballot(live), mi = __ballot(ins);
-      const uint32_t n = (uint32_t)__popcll(ml);
+      const uint32_t n = (uint32_t)__popcll(ml), lane = threadIdx.x & 63;
       const uint64_t slot0 = g->base + (uint32_t)__builtin_amdgcn_readlane((int)rank, 0);
       if (prefix_win && mi == ml && slot0 + n <= d.x_max) {
         // every live message of this wave commits and the window appends above every stored id (no
         // table insert): the wave's records are one run in the A buffer and one in the store, copied
-        // as 16 B words lane by lane (loaded above), so each load / store instruction covers one
-        // contiguous KiB (a record per lane put 64 lines into every instruction, every store a partial line)
+        // as 16 B words lane by lane, so each load / store instruction covers one contiguous KiB (a
+        // record per lane put 64 lines into every instruction, and every store was a partial line)
+        const uint4* src0 = reinterpret_cast<const uint4*>(rb.a_recv + rt_off_a(L, sg) + RT_HDR_A + (uint64_t)(k - lane) * 128);
         uint4* dst0 = reinterpret_cast<uint4*>(d.xr + slot0);
+        uint4 v[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) v[j] = lane + 64 * j < n * 8 ? src0[lane + 64 * j] : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++)
-          if (lane + 64 * j < n * 8) st_stream(dst0 + lane + 64 * j, in_v[j]);
+          if (lane + 64 * j < n * 8) st_stream(dst0 + lane + 64 * j, v[j]);
         if (ins) d.xstatus[slot] = 0;
       } else if (ins && sh_guard(g, slot < d.x_max, 5, slot)) {
         uint4 r[8];

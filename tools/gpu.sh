@@ -9,6 +9,7 @@
 #                                          tools/pmc_summary.py into pmc_NAME.json
 #   tools/gpu.sh pmcx NAME "CTRS" [bench args]  one PMC pass with the given counters (tools/pmc_counters.py)
 #   tools/gpu.sh profpy NAME script [args] the same passes over any script (e.g. tools/rehearse_shards.py)
+#   tools/gpu.sh pmcpy NAME "CTRS" script [args]  one PMC pass with the given counters over any script
 #   tools/gpu.sh rehearse NAME [args]      tools/rehearse_shards.py -> rehearse_NAME.json
 #   tools/gpu.sh py NAME script [args]     any probe script (tools/*.py) -> NAME.json
 #   tools/gpu.sh trace NAME script [args]  rocprofv3 kernel trace + stats of a script -> trace_NAME/
@@ -60,6 +61,12 @@ step() {
       mkdir -p $d
       timeout -s KILL 300 rocprofv3 --pmc $ctrs --output-format csv -d $d -o run -- python3 bench.py $B "$@" --no-phase-timing > $d/run.log 2>&1 || { echo "pmcx $name failed"; tail -3 $d/run.log; return 1; }
       python tools/pmc_counters.py $d > $out/pmcx_$name.json && head -c 800 $out/pmcx_$name.json; echo ;;
+    pmcpy)  # NAME "COUNTERS" script [args]: one PMC pass with the given counters over any script
+      local name=$1 ctrs=$2; shift 2
+      local d=$out/pmcx_$name
+      mkdir -p $d
+      timeout -s KILL 300 rocprofv3 --pmc $ctrs --output-format csv -d $d -o run -- python3 -u "$@" > $d/run.log 2>&1 || { echo "pmcpy $name failed"; tail -3 $d/run.log; return 1; }
+      python tools/pmc_counters.py $d > $out/pmcx_$name.json && head -c 1500 $out/pmcx_$name.json; echo ;;
     profpy)
       local name=$1; shift
       pmc_passes $name python3 -u "$@" || return 1 ;;
