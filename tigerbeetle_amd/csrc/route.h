@@ -151,8 +151,6 @@ struct RtBufs {
   unsigned long long* amt;  // owner: 64 slots x {low 32 bits, the rest} of the received amounts' sum
   uint32_t* hv;             // [0] the home verdict (k_rt_scan -> k_rt_decide)
   u128* imax;               // owner: per k_rt_own id block, the largest received transfer id
-  unsigned long long* lb;   // k_rt_route: per logical block and column, {epoch, flag, value} (look-back)
-  uint32_t* ticket;         // k_rt_route: the next logical block (the last one resets it)
 };
 
 __device__ inline uint32_t rt_lane_lt(unsigned long long m) {
@@ -413,210 +411,6 @@ __global__ void __launch_bounds__(RT_RT) k_rt_route2(Dev d, Scratch s, RtBufs rb
       m[1] = make_uint4((uint32_t)amount, (uint32_t)(amount >> 32), 1u, 0u);
     }
   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_rt_route (home, the default): k_rt_route1 + k_rt_scan + k_rt_route2 in one pass. Each block takes
-// the next logical block by ticket (so every block it waits on is running or done), validates and
-// routes its 256 events, publishes its per-destination message counts and then its inclusive
-// prefixes (decoupled look-back over the earlier blocks' published words, one lane per column), and
-// writes its messages from the record it still holds: the home slice is read once and two launches
-// go away. The last logical block writes the A headers and the home verdict (what k_rt_scan did).
-// A look-back that waits too long gives up: the window is rejected (the general path commits it).
-// ------------------------------------------------------------------------------------------------
-#define RT_LB_T 256
-#define RT_LB_COLS (2 * RT_MAXG + 1)  // per destination: id, side messages; then the OR of the verdict bits
-#define RT_LB_SPIN (1u << 22)
-enum : uint32_t { LB_AGG = 1, LB_PRE = 2 };
-__device__ inline unsigned long long rt_lb_word(uint32_t epoch, uint32_t flag, uint32_t v) {
-  return ((unsigned long long)epoch << 32) | ((unsigned long long)flag << 30) | (v & 0x3FFFFFFFu);
-}
-
-template <bool XFER>
-__global__ void __launch_bounds__(RT_LB_T) k_rt_route(Dev d, Scratch s, RtBufs rb, const uint8_t* __restrict__ ev_bytes,
-                                                      WinDesc w, RtLayout L, uint32_t nblk, uint64_t t_last,
-                                                      uint64_t first_ts, uint32_t multi, uint32_t epoch) {
-  __shared__ uint32_t sh_bl, laux, lgave;
-  __shared__ uint32_t wcnt[RT_LB_T / 64][RT_MAXG * 2];
-  __shared__ uint32_t lbase[RT_LB_COLS], ltot[RT_LB_COLS];
-  const uint32_t G = L.G, me = L.me, ncol = 2 * G, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (threadIdx.x == 0) {
-    sh_bl = atomicAdd(rb.ticket, 1u);
-    laux = 0;
-    lgave = 0;
-  }
-  __syncthreads();
-  const uint32_t bl = sh_bl, i = bl * RT_LB_T + threadIdx.x;
-  if (threadIdx.x == 0 && (i & (SEG - 1)) == 0) s.cnt_bad[i / SEG] = 0;  // (k_rt_decide adds to it)
-  // ---- k_rt_route1's part: stamp, static validation, owners ----
-  bool reach = false;
-  uint32_t o_id = 0, o_dr = 0, o_cr = 0, aux = 0;
-  uint4 r[8];
-  if (i < w.E) {
-    const uint4* q = reinterpret_cast<const uint4*>(ev_bytes + (size_t)i * 128);
-#pragma unroll
-    for (int k = 0; k < 8; k++) r[k] = q[k];
-    uint32_t cls = 0, code;
-    const uint32_t b = win_batch(w, i);
-    const tb_uint128_t id = rw_u128(r[0]);
-    if (XFER) {
-      tb_transfer_t t = *reinterpret_cast<const tb_transfer_t*>(r);
-      bool unsup = false;
-      code = sh_static_ct(t, w, b, i, &cls, &reach, &unsup);
-      if (unsup) aux |= RV_UNSUP;
-      if (reach && (uint64_t)(U(t.amount) >> 64) != 0) aux |= RV_HUGE;
-      s.id_tslot[i] = t.ledger;
-      if (i > 0 && !(U(id) > U(reinterpret_cast<const tb_transfer_t*>(ev_bytes)[i - 1].id))) aux |= RH_NONMONO << 8;
-    } else {
-      const tb_account_t a = *reinterpret_cast<const tb_account_t*>(r);
-      code = sh_static_ca(a, &cls, &reach);
-    }
-    if (reach) {
-      o_id = shard_of(id.lo, id.hi, G);
-      if (XFER) {
-        const tb_uint128_t dra = rw_u128(r[1]), cra = rw_u128(r[2]);
-        o_dr = shard_of(dra.lo, dra.hi, G);
-        o_cr = shard_of(cra.lo, cra.hi, G);
-      }
-    }
-    s.code[i] = reach ? CONT : code;
-    s.cls[i] = o_id | (o_dr << 4) | (o_cr << 8) | (reach ? RC_REACH : 0u) | ((cls & C_LINKED) ? RC_LINKED : 0u);
-    rw_stamp(r, win_ts(w, b, i));
-  }
-  // ---- ranks within the wave (ballots), counts per wave and destination ----
-  uint32_t r_id = 0, r_dr = 0, r_cr = 0;
-  for (uint32_t dd = 0; dd < G; dd++) {
-    const unsigned long long bi = __ballot(reach && o_id == dd);
-    if (o_id == dd) r_id = rt_lane_lt(bi);
-    uint32_t ns = 0;
-    if (XFER) {
-      const unsigned long long bd = __ballot(reach && o_dr == dd), bc = __ballot(reach && o_cr == dd);
-      const uint32_t before = rt_lane_lt(bd) + rt_lane_lt(bc);
-      if (o_dr == dd) r_dr = before;
-      if (o_cr == dd) r_cr = before + (o_dr == dd ? 1u : 0u);
-      ns = (uint32_t)(__popcll(bd) + __popcll(bc));
-    }
-    if (lane == 0) {
-      wcnt[wave][dd * 2] = (uint32_t)__popcll(bi);
-      wcnt[wave][dd * 2 + 1] = ns;
-    }
-  }
-  if (aux) atomicOr(&laux, aux);
-  __syncthreads();
-  // ---- publish this block's counts, look back over the earlier blocks, publish the prefixes ----
-  if (threadIdx.x < ncol + 1) {
-    const uint32_t col = threadIdx.x == ncol ? RT_LB_COLS - 1 : threadIdx.x;  // (the last lane: the verdict bits)
-    const bool orcol = threadIdx.x == ncol;
-    uint32_t own = 0;
-    if (orcol) own = laux;
-    else
-      for (uint32_t w2 = 0; w2 < RT_LB_T / 64; w2++) own += wcnt[w2][col];
-    unsigned long long* my = rb.lb + (size_t)bl * RT_LB_COLS + col;
-    uint32_t excl = 0;
-    if (bl == 0) {
-      __hip_atomic_store(my, rt_lb_word(epoch, LB_PRE, own), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(my, rt_lb_word(epoch, LB_AGG, own), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int64_t p = (int64_t)bl - 1; p >= 0; p--) {
-        const unsigned long long* q = rb.lb + (size_t)p * RT_LB_COLS + col;
-        unsigned long long wv = 0;
-        uint32_t tries = 0;
-        for (;;) {
-          wv = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((uint32_t)(wv >> 32) == epoch && ((wv >> 30) & 3u)) break;
-          if (++tries > RT_LB_SPIN) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (tries > RT_LB_SPIN) {
-          atomicOr(&lgave, 1u);
-          break;
-        }
-        const uint32_t v = (uint32_t)wv & 0x3FFFFFFFu;
-        excl = orcol ? (excl | v) : excl + v;
-        if (((wv >> 30) & 3u) == LB_PRE) break;
-      }
-      __hip_atomic_store(my, rt_lb_word(epoch, LB_PRE, orcol ? (excl | own) : excl + own), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    lbase[col] = excl;
-    ltot[col] = orcol ? (excl | own) : excl + own;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && lgave) rb.hv[1] = epoch;  // (k_rt_decide rejects the window)
-  // ---- k_rt_route2's part: the messages, in event order per destination ----
-  if (reach) {
-    uint32_t k_id = lbase[o_id * 2] + r_id, k_dr = 0, k_cr = 0;
-    for (uint32_t w2 = 0; w2 < wave; w2++) k_id += wcnt[w2][o_id * 2];
-    if (XFER) {
-      k_dr = lbase[o_dr * 2 + 1] + r_dr;
-      k_cr = lbase[o_cr * 2 + 1] + r_cr;
-      for (uint32_t w2 = 0; w2 < wave; w2++) {
-        k_dr += wcnt[w2][o_dr * 2 + 1];
-        k_cr += wcnt[w2][o_cr * 2 + 1];
-      }
-    }
-    reinterpret_cast<uint4*>(s.amt)[i] = make_uint4(k_id, k_dr, k_cr, 0);
-    const uint64_t ab = rt_blk_a(L, me);
-    if (k_id < L.c1[me]) {
-      uint4* dst = reinterpret_cast<uint4*>(rb.a_send + o_id * ab + RT_HDR_A + (uint64_t)k_id * 128);
-#pragma unroll
-      for (int k = 0; k < 8; k++) dst[k] = r[k];
-    }
-    if (XFER) {
-      const uint64_t amount = rw_u64(r[3].x, r[3].y);
-      const uint64_t side0 = RT_HDR_A + (uint64_t)L.c1[me] * 128;
-      if (k_dr < L.c2[me]) {  // RtSide: the account id, then {amount, side}
-        uint4* m = reinterpret_cast<uint4*>(rb.a_send + o_dr * ab + side0 + (uint64_t)k_dr * 32);
-        m[0] = r[1];
-        m[1] = make_uint4((uint32_t)amount, (uint32_t)(amount >> 32), 0u, 0u);
-      }
-      if (k_cr < L.c2[me]) {
-        uint4* m = reinterpret_cast<uint4*>(rb.a_send + o_cr * ab + side0 + (uint64_t)k_cr * 32);
-        m[0] = r[2];
-        m[1] = make_uint4((uint32_t)amount, (uint32_t)(amount >> 32), 1u, 0u);
-      }
-    }
-  }
-  if (bl != nblk - 1) return;
-  // ---- the last logical block: k_rt_scan's part (totals, A headers, home verdict, resets) ----
-  const uint64_t cb = rt_blk_c(L, me), ch = rt_c_hdr(L, me);
-  for (uint32_t dd = 0; dd < G; dd++) {
-    uint32_t* h = reinterpret_cast<uint32_t*>(rb.c_send + dd * cb);
-    for (uint32_t k = threadIdx.x; k < ch / 4; k += RT_LB_T) h[k] = 0;
-  }
-  for (uint32_t k = threadIdx.x; k < 128; k += RT_LB_T) rb.amt[k] = 0;
-  if (threadIdx.x != 0) return;
-  __hip_atomic_store(rb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (every block has its ticket)
-  const uint32_t vbits = ltot[RT_LB_COLS - 1];
-  uint32_t v = vbits & 0xFFu;
-  const bool nonmono = (vbits >> 8) & RH_NONMONO;
-  const uint32_t E = w.E;
-  // a pulse due inside the window (the caller ran the one before its first batch): outside the class
-  if (t_last >= d.g->pulse_next || (multi && t_last >= first_ts + TB_NS_PER_S)) v |= RV_PULSE;
-  uint64_t f0 = 0, f1 = 0, l0 = 0, l1 = 0;
-  if (E) {
-    const uint64_t* fr = reinterpret_cast<const uint64_t*>(ev_bytes);
-    const uint64_t* lr = reinterpret_cast<const uint64_t*>(ev_bytes + (size_t)(E - 1) * 128);
-    f0 = fr[0];
-    f1 = fr[1];
-    l0 = lr[0];
-    l1 = lr[1];
-  }
-  const uint64_t ab = rt_blk_a(L, me);
-  for (uint32_t dd = 0; dd < G; dd++) {
-    if (ltot[dd * 2] > L.c1[me] || ltot[dd * 2 + 1] > L.c2[me]) v |= RV_CAP;  // (none was written past it)
-    RtHdrA h;
-    h.n_id = min(ltot[dd * 2], L.c1[me]);
-    h.n_side = min(ltot[dd * 2 + 1], L.c2[me]);
-    h.n_home = E;
-    h.flags = (nonmono ? RH_NONMONO : 0u) | (E ? RH_NONEMPTY : 0u);
-    h.first_lo = f0;
-    h.first_hi = f1;
-    h.last_lo = l0;
-    h.last_hi = l1;
-    *reinterpret_cast<RtHdrA*>(rb.a_send + dd * ab) = h;
-  }
-  rb.hv[0] = v;
 }
 
 // The global facts every shard derives identically from the G A headers it received: the window's ids
@@ -900,8 +694,7 @@ __device__ inline uint32_t rt_code(const Scratch& s, const RtBufs& rb, const RtL
 }
 
 template <bool XFER>
-__global__ void __launch_bounds__(RT_DEC_T) k_rt_decide(Dev d, Scratch s, RtBufs rb, WinDesc w, RtLayout L,
-                                                         uint32_t epoch) {
+__global__ void __launch_bounds__(RT_DEC_T) k_rt_decide(Dev d, Scratch s, RtBufs rb, WinDesc w, RtLayout L) {
   __shared__ uint32_t nbad, vsh;
   __shared__ uint32_t cmin[RT_MAXG], ccnt[RT_MAXG][2];  // per destination: the block's first chunk, counts
   const uint32_t G = L.G, me = L.me;
@@ -920,7 +713,6 @@ __global__ void __launch_bounds__(RT_DEC_T) k_rt_decide(Dev d, Scratch s, RtBufs
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
     v |= rb.hv[0];
-    if (rb.hv[1] == epoch) v |= RV_CAP;  // k_rt_route's look-back gave up: the offsets are not trusted
     if (v && threadIdx.x < G) atomicOr(reinterpret_cast<uint32_t*>(rb.c_send + threadIdx.x * cb), v);
   }
   __syncthreads();
