@@ -666,8 +666,10 @@ def main():
             torch.cuda.set_device(local_rank % torch.cuda.device_count())
             dist.init_process_group("gloo")
         else:
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            # (TBG_RANKS_SHARE_GPU: a one-GPU rehearsal of the RCCL leg, every rank on device 0)
+            dev_idx = local_rank % torch.cuda.device_count() if os.environ.get("TBG_RANKS_SHARE_GPU") else local_rank
+            torch.cuda.set_device(dev_idx)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
     else:
         torch.cuda.set_device(0)
     device = torch.cuda.current_device()
@@ -889,6 +891,10 @@ def main():
                         "gpu_ms_timed": round(gpu_ms, 3), "wall_ms_timed": round(wall * 1000, 3)},
             "roofline": roof,
         }
+        if os.environ.get("TBG_BENCH_DBG"):  # the engine's instrumentation counters (tbg_debug_counters)
+            dbg = (ctypes.c_uint64 * 8)()
+            L.tbg_debug_counters(sm.h, dbg, 8)
+            line["results"]["debug_counters"] = list(dbg)
         if args.host_fed_transfers and cfg in ("cfg1", "cfg2") and world == 1:
             sm.prepare_timestamp = prepare_ts
             line["host_fed"] = host_fed(args, sm, torch, n_xfer, n_acc, seed, win)

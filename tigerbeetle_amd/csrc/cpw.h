@@ -16,6 +16,11 @@
 // region). The window's sequential walker is skipped; k_walk only folds the outcomes.
 #pragma once
 #include "walker.h"
+#ifndef CPS_PROF
+#define CPS_PROF_WALK_OFF 0
+#else
+#define CPS_PROF_WALK_OFF CPS_PROF
+#endif
 
 __device__ inline bool cpw_active(const Globals* g) {
   // windows with history rows need the exact balances after each event: sequential walker
@@ -47,9 +52,13 @@ __device__ inline void cc_union(uint32_t* parent, uint32_t a, uint32_t b) {
 
 __global__ void __launch_bounds__(256) k_cc_init(Dev d, Scratch s, uint32_t E) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) d.g->cc_count = 0;
+  if (i == 0) {
+    d.g->cc_count = 0;
+    d.g->cps_lists = 0;
+  }
   if (i >= E || !cpw_active(d.g)) return;
   s.cc_parent[i] = i;
+  s.rkey_in[i] = 0;  // (grouped form: the per-root counts)
 }
 
 __global__ void __launch_bounds__(256) k_cc_link(Dev d, Scratch s, WinDesc w, uint32_t epoch) {
@@ -99,10 +108,117 @@ __global__ void __launch_bounds__(1024) k_cc_segs(Dev d, Scratch s, uint32_t E) 
   if (start) s.cc_list[base + r] = k;
 }
 
+// Grouping W by component without a sort (the form used while cps.h takes the long components):
+// the W events counted per root, the roots' offsets from one scan, the events scattered to their
+// root's segment. A segment's order is then arbitrary; its walker (up to CC_REG events, in registers)
+// or its solver (in LDS) orders it by window position before walking. The onesweep sort this
+// replaces cost ~170 us per 1M-event window with its fills (k_cc_keys + sort + k_cc_segs).
+#define CC_REG 16
+__global__ void __launch_bounds__(256) k_cc_count(Dev d, Scratch s, uint32_t E) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E || !cpw_active(d.g) || !(s.cls[i] & C_W)) return;
+  const uint32_t r = cc_find(s.cc_parent, i);
+  s.rkey[i] = r;
+  atomicAdd(&s.rkey_in[r], 1u);
+}
+
+// Per 1024 roots: the number of W events and of components (packed: events | components << 21).
+__global__ void __launch_bounds__(1024) k_cc_bsum(Dev d, Scratch s, uint32_t E) {
+  __shared__ uint32_t lds[1024 / 64];
+  if (!cpw_active(d.g)) return;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = r < E ? s.rkey_in[r] : 0u;
+  const uint32_t v = block_sum<1024 / 64>(c | (c ? 1u << 21 : 0u), lds);
+  if (threadIdx.x == 0) s.rval_in[E + blockIdx.x] = v;
+}
+
+// Each root's segment offset (left in rkey_in as the scatter's cursor) and, per component in root
+// order, its start (cc_list) and length (Scratch::light, by component: no resolver runs in a
+// component-walked window).
+__global__ void __launch_bounds__(1024) k_cc_place(Dev d, Scratch s, uint32_t E) {
+  __shared__ uint32_t lds[1024 / 64];
+  if (!cpw_active(d.g)) return;
+  uint32_t pe = 0, pc = 0;  // W events and components of the earlier blocks' roots
+  for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) {
+    const uint32_t v = s.rval_in[E + b];
+    pe += v & 0x1FFFFFu;
+    pc += v >> 21;
+  }
+  pe = block_sum<1024 / 64>(pe, lds);
+  pc = block_sum<1024 / 64>(pc, lds);
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = r < E ? s.rkey_in[r] : 0u;
+  uint32_t tot;
+  const uint32_t ex = block_excl<1024 / 64>(c | (c ? 1u << 21 : 0u), lds, &tot);
+  const uint32_t off = pe + (ex & 0x1FFFFFu);
+  if (c) {
+    const uint32_t j = pc + (ex >> 21);
+    s.cc_list[j] = off;
+    s.light[j] = c;
+    s.rkey_in[r] = off;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.g->cc_count = pc + (tot >> 21);
+}
+
+__global__ void __launch_bounds__(256) k_cc_scatter(Dev d, Scratch s, uint32_t E) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E || !cpw_active(d.g) || !(s.cls[i] & C_W)) return;
+  s.rval[atomicAdd(&s.rkey_in[s.rkey[i]], 1u)] = i;
+}
+
+// A grouped segment in window order, by its walker thread: up to CC_REG events sorted in registers,
+// longer ones (components the solver does not take) by an in-place heap sort.
+__device__ inline void cc_order(uint32_t* seg, uint32_t len) {
+  if (len <= CC_REG) {
+    uint32_t v[CC_REG];
+#pragma unroll
+    for (int k = 0; k < CC_REG; k++) v[k] = (uint32_t)k < len ? seg[k] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int size = 2; size <= CC_REG; size <<= 1)
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+        for (int x = 0; x < CC_REG / 2; x++) {
+          const int lo = 2 * stride * (x / stride) + (x % stride), hi = lo + stride;
+          const bool up = (lo & size) == 0;
+          const uint32_t a = v[lo], b = v[hi];
+          const bool sw = (a > b) == up;
+          v[lo] = sw ? b : a;
+          v[hi] = sw ? a : b;
+        }
+#pragma unroll
+    for (int k = 0; k < CC_REG; k++)
+      if ((uint32_t)k < len) seg[k] = v[k];
+    return;
+  }
+  auto sift = [&](uint32_t root, uint32_t n) {
+    for (;;) {
+      uint32_t c = 2 * root + 1;
+      if (c >= n) return;
+      if (c + 1 < n && seg[c + 1] > seg[c]) c++;
+      if (seg[root] >= seg[c]) return;
+      const uint32_t t = seg[root];
+      seg[root] = seg[c];
+      seg[c] = t;
+      root = c;
+    }
+  };
+  for (uint32_t r = len / 2; r-- > 0;) sift(r, len);
+  for (uint32_t n = len; n > 1; n--) {
+    const uint32_t t = seg[0];
+    seg[0] = seg[n - 1];
+    seg[n - 1] = t;
+    sift(0, n - 1);
+  }
+}
+
 // One walker per component: events rval[start .. start + len), undo records from 5 * start (the
 // length from the component's last sorted position, k_cc_segs: no scan of the sorted keys).
+// Components of more than solve_min and at most solve_max events are cps.h's (solve_min 0: none).
+// grouped: the segments came from k_cc_place / k_cc_scatter (length in light[j], order by cc_order).
 template <bool XFER>
-__global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t* ev, WinDesc w, uint32_t epoch) {
+__global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t* ev, WinDesc w, uint32_t epoch,
+                                                 uint32_t solve_min, uint32_t solve_max, uint32_t grouped) {
   Globals* g = d.g;
   if (!cpw_active(g)) return;
   __shared__ uint2 pcache[256 * WCACHE];
@@ -112,7 +228,7 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
   uint32_t start = 0, len = 0;
   if (on) {
     start = s.cc_list[j];
-    len = s.light[s.rkey[start]] + 1 - start;
+    len = grouped ? s.light[j] : s.light[s.rkey[start]] + 1 - start;
   }
   // statistics (tbg_debug_counters): [5] longest component, [6] components, [7] W events walked;
   // one lane per block adds (same-address atomics from every wave serialize at the memory side)
@@ -133,12 +249,13 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
     atomicAdd(&st_sum, sum);
   }
   __syncthreads();
-  if (threadIdx.x == 0 && st_n) {
+  if (threadIdx.x == 0 && st_n && !CPS_PROF_WALK_OFF) {
     atomicMax((unsigned long long*)&g->dbg[5], (unsigned long long)st_mx);
     atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)st_n);
     atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)st_sum);
   }
-  if (!on) return;
+  if (!on || (solve_min && len > solve_min && len <= solve_max)) return;
+  if (grouped) cc_order(s.rval + start, len);
   uint2* mine = pcache + threadIdx.x * WCACHE;
   for (int k = 0; k < WCACHE; k++) mine[k] = make_uint2(NONE32, 0);
   Walker wk;

@@ -143,7 +143,7 @@ struct __attribute__((aligned(64))) Globals {
   uint32_t fu_epoch;    // the window k_ct_fused ran for (not backed off)
   uint32_t fu_prefix;   // that window extends the sorted prefix (captured before k_fu_final updates it)
   uint64_t fu_base;     // that window's first record slot
-  uint64_t pad7;
+  uint64_t cps_lists;  // cps.h this window: components listed, small class | large class << 32 (k_cc_init resets)
   uint64_t fu_windows;  // cumulative windows committed by the fused pass
   uint32_t fu_fail_epoch;  // the fused-only window that left the class (window_error bit 3)
   uint32_t sh_mis;         // sharded: this shard's ledger-mismatch slots used this window (shard.h)

@@ -784,6 +784,7 @@ __global__ void __launch_bounds__(256) k_classify(Dev d, Scratch s, WinDesc w, u
 }
 
 #include "cpw.h"
+#include "cps.h"
 
 // ------------------------------------------------------------------------------------------------
 // The ordered W list (one event per thread, one 1024-event segment per block; k_classify counted).
