@@ -153,6 +153,7 @@ struct Scratch {
   uint32_t* xw_cnt;             // [MAXB]
   unsigned long long* xw_tree;  // [2 * MAXB]
   unsigned long long* xw_minx;  // [MAXB]
+  unsigned long long* xw_ccnt;  // [MAXB] reset candidates per batch (k_xwin_pm)
   unsigned long long* xw_miny;  // [MAXB]
   uint64_t* pn_min;
   uint32_t* pn_res;

@@ -146,51 +146,119 @@ __global__ void __launch_bounds__(256) k_xwin_minlive(Dev d, Scratch s, WinDesc 
 
 #define XW_THREADS 1024
 
-// pulse_next_timestamp through the window, batch by batch (one workgroup).
-__global__ void __launch_bounds__(XW_THREADS) k_xwin_replay(Dev d, Scratch s, WinDesc w) {
+// The replay's reset candidates, per batch (one block each): a post/void op (value v, a pending
+// transfer's expires_at) resets pulse_next where v == min(pn, pm), pm the smallest creation value of
+// the batch before it (k_pn's "before"); only v <= pm can ever qualify, and only whether a batch
+// resets matters. So each candidate is kept as one word: v, with bit 63 set when v == pm (it resets
+// iff pm <= pn; otherwise iff v == pn). Listed per batch from its first event's position in the t2
+// area (free after k_final); values stay below 2^63 (TB_TIMESTAMP_MAX).
+#define XW_CAND_EQ (1ull << 63)
+__global__ void __launch_bounds__(XW_THREADS) k_xwin_pm(Dev d, Scratch s, WinDesc w) {
   __shared__ unsigned long long ldsm[XW_THREADS / 64];
-  __shared__ uint32_t first_eff;
-  // the per-batch tables in LDS (one coalesced load), so the batch-by-batch walk below pays no
-  // dependent global load per batch (the segment-tree path alone was 8 of them)
+  __shared__ uint32_t lds[XW_THREADS / 64];
+  if (WIN_REJECTED(d.g)) return;
+  const uint32_t b = blockIdx.x;
+  if (s.xw_miny[b] == ~0ull) {  // (k_xwin_minlive: no post/void op in the batch ran ok)
+    if (threadIdx.x == 0) s.xw_ccnt[b] = 0;
+    return;
+  }
+  unsigned long long* cv = reinterpret_cast<unsigned long long*>(s.t2);
+  unsigned long long carry = ~0ull;
+  uint32_t nc = 0;
+  for (uint32_t c0 = w.off[b]; c0 < w.off[b + 1]; c0 += XW_THREADS) {
+    const uint32_t k = c0 + threadIdx.x;
+    uint64_t v = 0;
+    const uint32_t op = k < w.off[b + 1] ? pn_op(s, k, &v) : 0u;
+    unsigned long long tot;
+    const unsigned long long pm = umin64(carry, block_excl_min_u64<XW_THREADS / 64>(op == 1 ? v : ~0ull, ldsm, &tot));
+    const bool cand = op == 2 && v <= pm && v <= TB_TIMESTAMP_MAX;
+    uint32_t tc;
+    const uint32_t r = block_excl<XW_THREADS / 64>(cand ? 1u : 0u, lds, &tc);
+    if (cand) cv[w.off[b] + nc + r] = v | (v == pm ? XW_CAND_EQ : 0ull);
+    nc += tc;
+    carry = umin64(carry, tot);
+  }
+  if (threadIdx.x == 0) s.xw_ccnt[b] = nc;
+}
+
+#define XW_LDS_CAND 4096  // candidates the replay holds in LDS (the rest are read from the t2 area)
+
+// pulse_next_timestamp through the window, batch by batch (one workgroup): a batch resets it if any
+// of its candidates qualifies (k_xwin_pm), else its creations lower it to minx. The candidates go to
+// LDS first, so the batch loop has no dependent global load.
+__global__ void __launch_bounds__(XW_THREADS) k_xwin_replay(Dev d, Scratch s, WinDesc w) {
   __shared__ unsigned long long tree[2 * MAXB], minx[MAXB], miny[MAXB];
+  __shared__ uint32_t coff[MAXB + 1];
+  __shared__ unsigned long long cl[XW_LDS_CAND];
   if (WIN_REJECTED(d.g)) return;
   for (uint32_t j = threadIdx.x; j < 2 * MAXB; j += XW_THREADS) tree[j] = s.xw_tree[j];
   for (uint32_t j = threadIdx.x; j < MAXB; j += XW_THREADS) {
     minx[j] = s.xw_minx[j];
     miny[j] = s.xw_miny[j];
   }
+  for (uint32_t b = threadIdx.x; b < w.nb; b += XW_THREADS) coff[b + 1] = (uint32_t)s.xw_ccnt[b];
+  __syncthreads();
+  if (threadIdx.x == 0) {  // (<= 128 batches, in LDS)
+    coff[0] = 0;
+    for (uint32_t b = 0; b < w.nb; b++) coff[b + 1] += coff[b];
+  }
+  __syncthreads();
+  const unsigned long long* cv = reinterpret_cast<const unsigned long long*>(s.t2);
+  // (flattened: candidate x of the window belongs to the batch b with coff[b] <= x < coff[b + 1])
+  const uint32_t held = min(coff[w.nb], (uint32_t)XW_LDS_CAND);
+  for (uint32_t x = threadIdx.x; x < held; x += XW_THREADS) {
+    uint32_t lo = 0, hi = w.nb;  // the last b with coff[b] <= x
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (coff[mid] <= x) lo = mid; else hi = mid;
+    }
+    cl[x] = cv[w.off[lo] + (x - coff[lo])];
+  }
+  __syncthreads();
+  // Per batch, in parallel: the value a pulse before it would set (the smallest entry live after it,
+  // from the segment tree), and whether the batch resets pulse_next when it starts from that value.
+  // The batch-by-batch loop below then only reads LDS words (it re-evaluates the candidates only for a
+  // batch that starts without a pulse).
+  __shared__ unsigned long long pv[MAXB];
+  __shared__ uint32_t rp[MAXB];
+  for (uint32_t b = threadIdx.x; b < w.nb; b += XW_THREADS) {
+    unsigned long long m = ~0ull;
+    for (uint32_t node = MAXB + b; node >= 1; node >>= 1) m = umin64(m, tree[node]);
+    pv[b] = m == ~0ull ? TB_TIMESTAMP_MAX : m;
+    rp[b] = 0;
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < coff[w.nb]; x += XW_THREADS) {
+    uint32_t lo = 0, hi = w.nb;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (coff[mid] <= x) lo = mid; else hi = mid;
+    }
+    const unsigned long long c = x < XW_LDS_CAND ? cl[x] : cv[w.off[lo] + (x - coff[lo])];
+    const unsigned long long v = c & ~XW_CAND_EQ, p0 = pv[lo];
+    if ((c & XW_CAND_EQ) ? v <= p0 : v == p0) rp[lo] = 1;
+  }
   __syncthreads();
   uint64_t pn = d.g->pulse_next;  // after the window's first pulse
   for (uint32_t b = 0; b < w.nb; b++) {
-    if (b >= 1 && pn <= w.T[b]) {
-      // the pulse before batch b: its finish takes the smallest entry live after it
-      unsigned long long m = ~0ull;
-      for (uint32_t node = MAXB + b; node >= 1; node >>= 1) m = umin64(m, tree[node]);
-      pn = m == ~0ull ? TB_TIMESTAMP_MAX : m;
-    }
-    if (miny[b] > pn) {  // no reset can take effect (it needs expires_at == pulse_next <= pn)
-      pn = umin64(pn, minx[b]);
-      continue;
-    }
     bool reset = false;
-    for (uint32_t c0 = w.off[b]; c0 < w.off[b + 1] && !reset; c0 += XW_THREADS) {
-      const uint32_t k = c0 + threadIdx.x;
-      uint64_t v = 0;
-      const uint32_t op = k < w.off[b + 1] ? pn_op(s, k, &v) : 0u;
-      unsigned long long tot;
-      const unsigned long long before = umin64(pn, block_excl_min_u64<XW_THREADS / 64>(op == 1 ? v : ~0ull, ldsm, &tot));
-      if (threadIdx.x == 0) first_eff = NONE32;
-      __syncthreads();
-      if (op == 2 && before == v) atomicMin(&first_eff, k);
-      __syncthreads();
-      if (first_eff != NONE32) {
-        pn = TB_TIMESTAMP_MIN;  // :1706-1707; the next batch's pulse check is true
-        reset = true;
-      } else {
-        pn = umin64(pn, tot);
+    if (b >= 1 && pn <= w.T[b]) {
+      pn = pv[b];  // the pulse before batch b: its finish takes the smallest entry live after it
+      reset = miny[b] <= pn && rp[b];
+    } else if (miny[b] <= pn) {  // (else no reset can take effect: it needs expires_at == pulse_next <= pn)
+      const uint32_t n = coff[b + 1] - coff[b];
+      for (uint32_t c0 = 0; c0 < n && !reset; c0 += XW_THREADS) {
+        const uint32_t j = c0 + threadIdx.x, x = coff[b] + j;
+        bool q = false;
+        if (j < n) {
+          const unsigned long long c = x < XW_LDS_CAND ? cl[x] : cv[w.off[b] + j];
+          const unsigned long long v = c & ~XW_CAND_EQ;
+          q = (c & XW_CAND_EQ) ? v <= pn : v == pn;
+        }
+        reset = __syncthreads_or(q ? 1 : 0) != 0;
       }
-      __syncthreads();
     }
+    pn = reset ? TB_TIMESTAMP_MIN : umin64(pn, minx[b]);  // (:1706-1707; the next batch's pulse check is true)
   }
   if (threadIdx.x == 0) d.g->pulse_next = pn;
 }
