@@ -666,10 +666,8 @@ def main():
             torch.cuda.set_device(local_rank % torch.cuda.device_count())
             dist.init_process_group("gloo")
         else:
-            # (TBG_RANKS_SHARE_GPU: a one-GPU rehearsal of the RCCL leg, every rank on device 0)
-            dev_idx = local_rank % torch.cuda.device_count() if os.environ.get("TBG_RANKS_SHARE_GPU") else local_rank
-            torch.cuda.set_device(dev_idx)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
     device = torch.cuda.current_device()
