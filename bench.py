@@ -134,7 +134,9 @@ def pmc_traffic(config, kernel, events_per_launch):
     k = ks.get(kernel) or ks.get(kernel.split("<")[0])  # (earlier rounds' summaries: untemplated names)
     if not k:
         return None
-    scale = events_per_launch / max(k["grid"], 1)
+    # per-event grids scale with this run's events per launch; a fixed grid (k_rc_run: one workgroup)
+    # reports the profiled launch as is
+    scale = events_per_launch / max(k["grid"], 1) if k["grid"] * 2 >= events_per_launch else 1.0
     return (round(k["traffic_bytes"] * scale), round(k["traffic_fetch_x2_bytes"] * scale),
             os.path.relpath(path, ROOT))
 
