@@ -444,6 +444,10 @@ __device__ uint32_t cps_component(const Dev& d, const Scratch& s, const uint8_t*
     cps_fpos<NT>(L, n);
     if (!__syncthreads_or(changed ? 1 : 0)) break;
   }
+  if (pass == 2 * n + 4) {  // (not reached: position k settles by pass 2k + 2) fail the window loudly
+    if (lane == 0) atomicOr(&d.g->window_error, 4u);
+    return pass;
+  }
   if (CPS_PROF) tp2 = wall_clock64();
   // 5. the walker's side effects
   for (uint32_t k = lane; k < n; k += NT) {
