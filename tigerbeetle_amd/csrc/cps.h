@@ -298,6 +298,14 @@ __device__ uint32_t cps_component(const Dev& d, const Scratch& s, const uint8_t*
         L.k1[k] = r0.z;
         if (cls & C_POSTVOID) L.k2[k] = r0.w;
       }
+      if (rs == 0xFF && !(cls & C_POSTVOID)) {
+        // a create: k_ct_prep's code is its outcome unless an earlier event committed its id (the
+        // stored-id exists check is static; else the zero-balance tail: ok or overflows_timeout)
+        if (r0.y != NONE32)
+          rs = r0.x;
+        else
+          L.bal[k] = (uint8_t)r0.x;
+      }
       L.rs[k] = (uint8_t)rs;
     }
   }
@@ -379,9 +387,8 @@ __device__ uint32_t cps_component(const Dev& d, const Scratch& s, const uint8_t*
     for (int u = 0; u < 2; u++) {
       const uint32_t k = k0 + NT * u;
       c0v[u] = CPS_N16;
-      if (k >= n || L.rs[k] != 0xFF) continue;
+      if (k >= n || L.rs[k] != 0xFF || !(L.cls[k] & C_POSTVOID)) continue;  // (creates: step 1)
       tv[u] = cps_event(ev, w, L, k);
-      if (!(L.cls[k] & C_POSTVOID)) continue;
       if (L.pslot[k] != NONE32) {
         c0v[u] = CPS_STORED;
       } else if (L.k2[k] != NONE32) {
@@ -396,18 +403,8 @@ __device__ uint32_t cps_component(const Dev& d, const Scratch& s, const uint8_t*
 #pragma unroll
     for (int u = 0; u < 2; u++) {
       const uint32_t k = k0 + NT * u;
-      if (k >= n || L.rs[k] != 0xFF) continue;
+      if (k >= n || L.rs[k] != 0xFF || !(L.cls[k] & C_POSTVOID)) continue;
       const tb_transfer_t& t = tv[u];
-      if (!(L.cls[k] & C_POSTVOID)) {
-        if (L.idts[k] != NONE32) {
-          L.rs[k] = (uint8_t)ct_exists(t, d.xr[L.idts[k]]);  // a stored transfer with this id: static
-        } else {
-          const Bal z = {0, 0, 0, 0};
-          u128 amount;
-          L.bal[k] = (uint8_t)ct_balances(t, z, 0, z, 0, &amount);
-        }
-        continue;
-      }
       const uint32_t c0 = c0v[u];
       if (c0 == CPS_STORED) L.pst0[k] = d.xstatus[L.pslot[k]];
       if (c0 == CPS_N16) continue;

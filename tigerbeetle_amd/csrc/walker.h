@@ -6,6 +6,10 @@
 #include "sm_logic.h"
 #include "window.h"
 
+#ifndef WALK_CREATE_ROW
+#define WALK_CREATE_ROW 1  // component walkers: creates decided from k_ct_prep's row (no record load)
+#endif
+
 // An entry the expires_at scan can return (composite key range, lsm/composite_key.zig:25-57).
 __device__ inline bool xw_visible(uint64_t timestamp, uint64_t expires_at) {
   return !(timestamp >> 63) && expires_at <= TB_TIMESTAMP_MAX;
@@ -233,7 +237,9 @@ struct Walker {
       e.cr = r1.y;
       e.p_tslot = r1.z;
       e.b = r1.w;
-      e.head = reinterpret_cast<const uint4*>(ev)[(size_t)i * 8];
+      // (a component walker loads an event's record only where it reads it: a create's outcome is
+      // k_ct_prep's code unless an earlier event of the window committed its id, WALK_CREATE_ROW)
+      if (!WALK_CREATE_ROW || !atomic_bal) e.head = reinterpret_cast<const uint4*>(ev)[(size_t)i * 8];
       e.id_alone = (e.cls & C_IDALONE) != 0;
       return e;
     }
@@ -266,9 +272,27 @@ struct Walker {
       pc = pcache_find(e.pid_ent);
       if (pc < 0) pc = bmap_committed(s.bmap, e.pid_ent, epoch);
     }
+    if (WALK_CREATE_ROW && atomic_bal && rows && !pv) {
+      // create in a component window: k_ct_prep's code is the walker's result (the stored-id exists
+      // check, else the zero-balance tail: ok or overflows_timeout; no balancing, no limits here)
+      // unless an earlier event of the window committed its id
+      if (e.id_tslot != NONE32) return e.code;
+      if (c >= 0) {
+        tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev)[i];
+        t.timestamp = win_ts(*w, e.b, i);
+        return ct_exists(t, walk_record(c));
+      }
+      if (e.code != TB_CT_OK) return e.code;
+      tb_transfer_t none;
+      commit_record(i, e.id_ent, none, false);  // (a component walker stores no record for a create)
+      if (e.cls & C_PENDING) s.bstatus[i] = TB_PENDING_PENDING;
+      return TB_CT_OK;
+    }
     tb_transfer_t t = reinterpret_cast<const tb_transfer_t*>(ev)[i];
-    t.id.lo = ((uint64_t)e.head.y << 32) | e.head.x;
-    t.id.hi = ((uint64_t)e.head.w << 32) | e.head.z;
+    if (!WALK_CREATE_ROW || !atomic_bal) {
+      t.id.lo = ((uint64_t)e.head.y << 32) | e.head.x;
+      t.id.hi = ((uint64_t)e.head.w << 32) | e.head.z;
+    }
     t.timestamp = win_ts(*w, e.b, i);
     if (pv) return post_or_void(e, t, c, pc);
     if (e.id_tslot != NONE32) return ct_exists(t, d.xr[e.id_tslot]);
