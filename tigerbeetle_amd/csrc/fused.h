@@ -114,8 +114,10 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
           const bool mx = x_may_exist(t.id, x_id_max);
           const uint64_t hx = hash_id(t.id.lo, t.id.hi);
           const AccEntry ed = d.acc_tab[hd], ec = d.acc_tab[hc];
-          // (claim mode probes whether or not the id may exist: its claim indexes the new record)
-          const XEntry ex = (mx || claim) ? d.x_tab[hx & d.x_mask] : X_EMPTY;
+          // (claim mode claims without reading the entry first: x_probe_claim's compare-and-swap
+          // returns what the entry holds, so the claim is one memory-side atomic on the 2 GB table
+          // instead of a line read plus the atomic)
+          const XEntry ex = (mx && !claim) ? d.x_tab[hx & d.x_mask] : X_EMPTY;
           AccEntry de, ce;
           o->dr = acc_probe_from(d.acc_tab, d.acc_mask, hd, ed, t.debit_account_id, &de);
           o->cr = acc_probe_from(d.acc_tab, d.acc_mask, hc, ec, t.credit_account_id, &ce);
@@ -143,8 +145,11 @@ __device__ __forceinline__ void fu_decide(const Dev& d, uint32_t i, u128 prev_id
               // the sorted prefix first (a transfer found there is not in the table), then the claim
               if (mx) xs = x_prefix_find(d.xr, P, t.id);
               bool dup = false;
-              if (xs == NONE32)
-                xs = x_probe_claim(d.x_tab, d.xr, ev, d.x_mask, hx, ex, t.id, base, i, E, !tovf, &dup, &o->cpos);
+              if (xs == NONE32) {
+                // (an event that will not insert must read the entry: it only looks for its id)
+                const XEntry e0 = tovf ? d.x_tab[hx & d.x_mask] : X_EMPTY;
+                xs = x_probe_claim(d.x_tab, d.xr, ev, d.x_mask, hx, e0, t.id, base, i, E, !tovf, &dup, &o->cpos);
+              }
               if (dup) simple = false;  // in-window duplicate
             } else {
               xs = mx ? x_probe_from(d.x_tab, d.xr, d.x_mask, hx, ex, t.id) : NONE32;
