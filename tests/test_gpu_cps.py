@@ -134,3 +134,31 @@ def test_cps_cfg4_window(monkeypatch, cps_min):
     finally:
         gpu.close()
         ref.close()
+
+
+@pytest.mark.gpu
+def test_cps_component_above_the_solver():
+    """A linked chain of 700 events (one component above CPS_NMAX = 512) in every window: the grouped
+    window walks it after cc_order's in-place sort, and the window after it is grouped by the sort
+    (cpw.h); replies and stores against the restatement."""
+    from tigerbeetle_amd import StateMachine
+
+    bm, n_acc = 2048, 2000
+    gpu = StateMachine(batch_max=bm, accounts_max=n_acc, transfers_max=1 << 16, window_events_max=2 * bm)
+    ref = OracleStateMachine(batch_max=bm)
+    try:
+        acc = [workload.accounts(0, n_acc, seed=5)]
+        assert commit_window(gpu, Operation.create_accounts, acc) == oracle_batches(ref, Operation.create_accounts, acc)
+        for w in range(4):
+            batches = [workload.transfers_cfg4((w * 2 + k) * bm, bm, 5, n_acc, bm) for k in range(2)]
+            b = batches[0]
+            b["flags"][:699] |= np.uint16(1)   # linked: events 0..698 chain into 699
+            b["flags"][699] &= ~np.uint16(1)
+            g = commit_window(gpu, Operation.create_transfers, batches)
+            r = oracle_batches(ref, Operation.create_transfers, batches)
+            assert g == r, f"window {w}"
+            assert gpu.pulse_next_timestamp() == ref.pulse_next_timestamp()
+        _compare_final(gpu, ref)
+    finally:
+        gpu.close()
+        ref.close()

@@ -55,6 +55,7 @@ __global__ void __launch_bounds__(256) k_cc_init(Dev d, Scratch s, uint32_t E) {
   if (i == 0) {
     d.g->cc_count = 0;
     d.g->cps_lists = 0;
+    d.g->cpw_want &= ~2u;  // (k_cc_walk: a component above CPS_NMAX this window)
   }
   if (i >= E || !cpw_active(d.g)) return;
   s.cc_parent[i] = i;
@@ -254,6 +255,9 @@ __global__ void __launch_bounds__(256) k_cc_walk(Dev d, Scratch s, const uint8_t
     atomicAdd((unsigned long long*)&g->dbg[6], (unsigned long long)st_n);
     atomicAdd((unsigned long long*)&g->dbg[7], (unsigned long long)st_sum);
   }
+  // a component too long for the solver: the host groups the next window by the sort (its segments
+  // come ordered), so a run of such windows pays cc_order's heap sort at most once
+  if (on && len > solve_max) atomicOr(&g->cpw_want, 2u);
   if (!on || (solve_min && len > solve_min && len <= solve_max)) return;
   if (grouped) cc_order(s.rval + start, len);
   uint2* mine = pcache + threadIdx.x * WCACHE;

@@ -826,7 +826,7 @@ __global__ void __launch_bounds__(WALK_THREADS) k_walk(Dev d, Scratch s, const u
   if (threadIdx.x == 0) {
     // the host launches the component walkers only while recent windows had W events they could
     // take (no hot account): balance-limit windows (resolver) skip their launches and sort
-    d.g->cpw_want = w_count != 0 && cpw_active(d.g) ? 1u : 0u;
+    d.g->cpw_want = (d.g->cpw_want & 2u) | (w_count != 0 && cpw_active(d.g) ? 1u : 0u);
   }
   if (w_count == 0) {
     if (threadIdx.x == 0) {
