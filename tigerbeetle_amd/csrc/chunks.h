@@ -34,8 +34,11 @@
 #define RC_EM_CHECK 0x800u
 #define RC_EM_ADD 0x1000u
 #ifndef RC_HEAD_SIMD
-#define RC_HEAD_SIMD 1  // 1: the chunk's longest segment walked by wave 0 alone on its SIMD; 2: by wave 0
-                        // (others share the SIMD); 0: taken from the long queue like any other
+// 1: the chunk's longest segment walked by wave 0 alone on its SIMD; 2: by wave 0 (others share the
+// SIMD); 0: taken from the long queue like any other. Round 6 (cfg3, one box): 0 9.87, 1 9.39,
+// 2 6.92 x 10^7 transfers/s — the other segments' walks, not the head's, pace an iteration
+// (RC_PROF: the longest wave walk is 0.78 of 1.84 ms of walk phases per window), so no wave sits out.
+#define RC_HEAD_SIMD 0
 #endif
 #ifndef RC_PROF
 #define RC_PROF 0  // 1: per-phase clock64() sums of k_rc_run into Globals::dbg (tbg_debug_counters);
