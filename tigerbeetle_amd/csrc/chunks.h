@@ -56,6 +56,7 @@
 //   rc_list[cb + i]    segment ids: the > 64-entry segments, then the > RC_LONG ones, then the rest
 //   rc_ent[2e + side]  the entry of (event e, side) within its chunk (RC_NONE: that side is not hot)
 //   rc_em[k]           entry k's encoding (RC_EM_*)
+//   rc_srank[cb + c + i] segment i's compact rank (its A without a load of its first entry's rank)
 //   rc_cnt[c]          (nseg, huge, long, some amount >= 2^24)
 // and per rank (from the first entry of each (chunk, rank) segment: identical values) its account
 // slot and initial A in rstate.
@@ -66,7 +67,7 @@ struct RcLds {
   int64_t delta[RC_ME];        // per segment: its effects on A (last walk)
   uint16_t em[RC_ME];          // entry encoding (RC_EM_*)
   uint32_t dfrom[RC_ME];       // per segment: first entry whose input changed (RC_NONE: clean)
-  uint16_t rank[RC_ME];
+  uint16_t srank[RC_ME];       // per segment: its account's compact rank (k_rc_build)
   uint16_t segof[RC_ME];       // entry -> segment
   uint16_t seg[RC_ME + 1];     // segment starts (entry index), seg[nseg] = entries
   uint16_t lst[RC_ME];         // segment ids: long ones (the longest first), then short ones
@@ -196,8 +197,14 @@ __global__ void __launch_bounds__(RC_T) k_rc_build(Dev d, Scratch s, uint32_t E)
   const unsigned long long upto = (2ull << lane) - 1ull;  // lanes <= this one
   const uint32_t id0 = pre0 + (uint32_t)__popcll(b0 & upto) - 1u;
   const uint32_t id1 = tot0 + pre1 + (uint32_t)__popcll(b1 & upto) - 1u;
-  if (f[0]) seg[id0] = (uint16_t)t;
-  if (f[1]) seg[id1] = (uint16_t)(t + RC_T);
+  if (f[0]) {
+    seg[id0] = (uint16_t)t;
+    s.rc_srank[cb0 + c + id0] = (uint16_t)(sk[t] >> 11);
+  }
+  if (f[1]) {
+    seg[id1] = (uint16_t)(t + RC_T);
+    s.rc_srank[cb0 + c + id1] = (uint16_t)(sk[t + RC_T] >> 11);
+  }
   if (t < m) s.rc_segof[cb0 + t] = (uint16_t)id0;
   if (t + RC_T < m) s.rc_segof[cb0 + t + RC_T] = (uint16_t)id1;
   const uint32_t nseg = tot0 + tot1;
@@ -327,7 +334,7 @@ __device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, int la
                                       uint64_t* tp) {
   const uint64_t e0 = RC_PROF == 2 ? clock64() : 0;
   const uint32_t s0 = rc_uniform(L.seg[sg]), s1 = rc_uniform(L.seg[sg + 1]);
-  const int64_t A0 = rc_uniform64(L.A[L.rank[s0]]);
+  const int64_t A0 = rc_uniform64(L.A[L.srank[sg]]);
   // a re-walk starts at the first entry whose input changed, from the balance kept before it
   int64_t D = kf == s0 ? 0 : rc_uniform64(L.dent[kf]);
   if (RC_PROF == 2) {  // walks and their set-up cycles
@@ -361,7 +368,7 @@ __device__ inline void rc_walk_wave32(RcLds& L, uint32_t sg, uint32_t kf, int la
 __device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t kf, int lane) {
   // wave-uniform bounds (SGPRs): the step loop and its ballots are uniform control flow
   const uint32_t s0 = rc_uniform(L.seg[sg]), s1 = rc_uniform(L.seg[sg + 1]);
-  const int64_t A0 = rc_uniform64(L.A[L.rank[s0]]);
+  const int64_t A0 = rc_uniform64(L.A[L.srank[sg]]);
   int64_t D = kf == s0 ? 0 : rc_uniform64(L.dent[kf]);
   for (uint32_t k = kf; k < s1; k += 64) {
     const uint32_t kk = k + (uint32_t)lane;
@@ -407,7 +414,7 @@ __device__ inline void rc_walk_wave(RcLds& L, uint32_t sg, uint32_t kf, int lane
 // short segments are only consumed as "walk it").
 __device__ inline void rc_walk_lane(RcLds& L, uint32_t sg) {
   const uint32_t s0 = L.seg[sg], s1 = L.seg[sg + 1];
-  const int64_t A0 = L.A[L.rank[s0]];
+  const int64_t A0 = L.A[L.srank[sg]];
   int64_t D = 0;
   for (uint32_t k = s0; k < s1; k++) {
     const uint32_t em = L.em[k];
@@ -446,10 +453,10 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
   for (uint32_t c = t; c < nch; c += RC_T) L.cb[c] = s.rc_cb[c];  // chunk ends (k_rc_build)
   __syncthreads();
   // the next chunk's entries and tables, loaded one chunk ahead (two of each per thread)
-  uint32_t pk[2] = {0, 0}, pe = 0;
+  uint32_t pe = 0;
   uint16_t pm[2] = {0, 0};
   uint64_t pa[2] = {0, 0};
-  uint16_t ps[2] = {0, 0}, pg[2] = {0, 0}, pl[2] = {0, 0};
+  uint16_t ps[2] = {0, 0}, pg[2] = {0, 0}, pl[2] = {0, 0}, pr[2] = {0, 0};
   uint4 pc = make_uint4(0, 0, 0, 0);
   auto fetch = [&](uint32_t c) {
     const uint32_t b0 = 2 * c * RC_C, b1 = L.cb[c];
@@ -459,11 +466,11 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
       const uint32_t kl = t + (uint32_t)j * RC_T;
       if (b0 + kl < b1) {
         pm[j] = s.rc_em[b0 + kl];
-        pk[j] = s.rkey[b0 + kl];
         pa[j] = (uint64_t)s.ramt[b0 + kl];
         ps[j] = s.rc_segof[b0 + kl];
         pl[j] = s.rc_list[b0 + kl];
       }
+      if (b0 + kl < b1) pr[j] = s.rc_srank[b0 + c + kl];  // (read past nseg too: unused there)
       if (b0 + kl <= b1) pg[j] = s.rc_seg[b0 + c + kl];
     }
     if (c * RC_C + t < E) pe = *(const uint32_t*)&s.rc_ent[2 * (c * RC_C + t)];
@@ -483,13 +490,13 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
       if (kl < m) {
         L.em[kl] = pm[j];
         L.amt[kl] = pa[j];
-        L.rank[kl] = (uint16_t)(pk[j] & RC_RMASK);
         L.segof[kl] = ps[j];
         L.oth[kl] = 1;
       }
       if (kl < nseg) {
         L.lst[kl] = pl[j];
         L.dfrom[kl] = pg[j];  // every segment is walked in the first iteration
+        L.srank[kl] = pr[j];
       }
       if (kl <= nseg) L.seg[kl] = pg[j];
     }
@@ -621,7 +628,7 @@ __global__ void __launch_bounds__(RC_T) k_rc_run(Dev d, Scratch s, uint32_t E) {
     }
     // the chunk is final: advance A, publish the statuses and the committed entries
     for (uint32_t sg = t; sg < nseg; sg += RC_T) {
-      const uint32_t r = L.rank[L.seg[sg]];
+      const uint32_t r = L.srank[sg];
       L.A[r] += L.delta[sg];
     }
     if (c0 + t < E) s.st[c0 + t] = (L.cur[t] ? ST_DR_PASS : 0u) | (L.cur[RC_C + t] ? ST_CR_PASS : 0u);

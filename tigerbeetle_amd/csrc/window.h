@@ -136,7 +136,7 @@ struct Scratch {
   // tables k_rc_build builds (segment of each entry, segment starts, walk lists, entry of each event
   // side, counts)
   uint32_t* rc_cb;
-  uint16_t *rc_segof, *rc_seg, *rc_list, *rc_ent, *rc_em;
+  uint16_t *rc_segof, *rc_seg, *rc_srank, *rc_list, *rc_ent, *rc_em;
   uint4* rc_cnt;
   // pulse_next (k_pn): per event the op's value (C_PNOP) and, for a walker post/void of a pending
   // transfer created in the window, that transfer's event index; per segment the min creation value
