@@ -27,7 +27,9 @@
 
 #define RC_T 1024  // threads of the workgroup
 #define RC_ME (2 * RC_C)  // entries per chunk at most
-#define RC_LONG 8  // longer segments are walked by a whole wave
+#ifndef RC_LONG
+#define RC_LONG 8  // longer segments are walked by a whole wave (round 6 A/B on cfg3: 4, 12 and 16 slower)
+#endif
 // Entry encoding in LDS (k_rc_build): bits 0-10 the (side, event) check slot (side << 10 | event in
 // chunk), bit 11 the entry's side checks (a limit), bit 12 a committed entry raises A.
 #define RC_EM_IDX 0x7FFu
